@@ -1,0 +1,992 @@
+// oracle/rt_oracle.cpp -- TEST INFRASTRUCTURE: CPU restatement of the reference ray tracer.
+//
+// This file is the parity oracle for the MI355X product path.  Only tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only as the
+// checker (or the timed CPU baseline) -- never as the thing measured or shipped.
+//
+// It restates, function by function, the reference's per-pixel path
+// (paths relative to /root/reference/Code/):
+//   compute_pixel_color        raytracer.cpp:18-70
+//   VecMath (+ reflect/refract, random_in_unit_sphere)   raytracer.cpp:74-173
+//   shade                      raytracer.cpp:180-274
+//   Trace                      raytracer.cpp:280-351
+//   pixel finalise (gamma)     raytracer.cpp:446-457, image.cpp:28-37, image.cpp:53-83
+//   Camera                     camera.cpp:14-58 (reader), camera.cpp:90-179 (thin lens)
+//   Shapes / AABB              shapes.cpp:1-503, shapes.hpp:1-140
+//   BVH                        acceleration.cpp:1-150
+//   loaders                    json_loader.cpp:30-338, material.hpp:12-134, image.cpp:86-133
+// with the random stream made injectable:
+//   * RNG_MT19937: one std::mt19937 seeded once, consumed serially in raster order exactly as
+//     main() does (raytracer.cpp:425-442; seed replaces std::random_device) -- this mode is
+//     pinned byte-for-byte against the compiled reference (oracle/_ref, tests/golden);
+//   * RNG_COUNTER: the same draw sequence, but each (pixel, sample) restarts a counter-based
+//     stream (splitmix64 keyed by seed/pixel/sample, draw index as counter).  This is the
+//     partition-independent stream the GPU kernel implements; GPU == oracle is checked in
+//     this mode.
+// Every float expression keeps the reference's operand order; build with -ffp-contract=off.
+#include <algorithm>
+#include <chrono>
+#include <array>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <limits>
+#include <memory>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "mini_json.hpp"
+#define RT_FMA64 std::fma
+#include "../ray_tracying_amd/csrc/common/rt_powf.h"  // glibc powf restatement (pinned vs libm)
+
+namespace orc {
+
+using V3 = std::array<float, 3>;
+
+// ---------------------------------------------------------------- Color / Material / Light
+// material.hpp:12-41
+struct Color {
+  float r = 0.0f, g = 0.0f, b = 0.0f;
+  Color operator+(const Color& o) const { return {r + o.r, g + o.g, b + o.b}; }
+  Color operator*(const Color& o) const { return {r * o.r, g * o.g, b * o.b}; }
+  Color operator*(float s) const { return {r * s, g * s, b * s}; }
+  Color operator/(float s) const { return {r / s, g / s, b / s}; }
+};
+inline Color operator*(float s, const Color& c) { return c * s; }
+
+// image.hpp/image.cpp: P3 texture reader (image.cpp:86-133) -- only the reading side.
+struct Texture {
+  int width = 0, height = 0;
+  bool loaded = false;
+  std::vector<unsigned> px;
+  explicit Texture(const std::string& fn) {
+    std::ifstream f(fn);
+    if (!f.is_open()) { std::cerr << "Error: Could not open file " << fn << " for reading\n"; return; }
+    std::string magic, line;
+    f >> magic;
+    if (magic != "P3") { std::cerr << "Error: Only P3 PPM format is supported\n"; return; }
+    f >> std::ws;
+    while (f.peek() == '#') { std::getline(f, line); f >> std::ws; }
+    f >> width >> height;
+    int maxc; f >> maxc;
+    px.assign((size_t)width * height * 3, 0);
+    for (int i = 0; i < width * height * 3; ++i) { int v = 0; f >> v; px[i] = (unsigned)std::max(0, std::min(v, 255)); }
+    loaded = true;
+  }
+  void get(int x, int y, int& r, int& g, int& b) const {
+    if (x < 0 || x >= width || y < 0 || y >= height) { r = g = b = 0; return; }
+    size_t i = ((size_t)y * width + x) * 3;
+    r = (int)px[i]; g = (int)px[i + 1]; b = (int)px[i + 2];
+  }
+};
+
+// material.hpp:47-134 (defaults of the C++ class, used when "material" is absent/invalid)
+struct Material {
+  Color diffuse_color = {0.8f, 0.8f, 0.8f};
+  Color specular_color = {1.0f, 1.0f, 1.0f};
+  float k_ambient = 0.1f, k_diffuse = 0.9f, k_specular = 0.3f, shininess = 20.0f;
+  float roughness = 0.0f, reflectivity = 0.0f, transparency = 0.0f, refractive_index = 1.0f;
+  std::shared_ptr<Texture> texture;
+  bool has_texture() const { return texture && texture->loaded; }
+  // material.hpp:99-134
+  Color diffuse(float u, float v) const {
+    if (!has_texture()) return diffuse_color;
+    int x = static_cast<int>(u * (texture->width - 1));
+    int y = static_cast<int>((1.0f - v) * (texture->height - 1));
+    int r, g, b;
+    texture->get(x, y, r, g, b);
+    Color t = {r / 255.0f, g / 255.0f, b / 255.0f};
+    return t * diffuse_color;
+  }
+};
+
+struct Light {  // light.hpp:5-13
+  V3 location, color;
+  float intensity, radius;
+};
+
+// ---------------------------------------------------------------- geometry (shapes.*)
+struct Ray {  // shapes.hpp:25-29
+  V3 origin{}, direction{};
+  float time = 0.0f;
+};
+struct Shape;
+struct Hit {  // shapes.hpp:15-23
+  V3 p{}, n{};
+  float t = 0.0f;
+  Shape* shape = nullptr;
+  float u = 0.0f, v = 0.0f;
+  int order = 0;  // position in the BVH-sorted shape list (diagnostics only)
+};
+
+static inline V3 vsub(const V3& a, const V3& b) { return {a[0] - b[0], a[1] - b[1], a[2] - b[2]}; }
+static inline V3 vcross(const V3& a, const V3& b) {
+  return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+}
+static inline float vdot(const V3& a, const V3& b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <class T> static inline const T& smax(const T& a, const T& b) { return (a < b) ? b : a; }  // std::max
+template <class T> static inline const T& smin(const T& a, const T& b) { return (b < a) ? b : a; }  // std::min
+
+struct AABB {  // shapes.hpp:31-58, shapes.cpp:46-86
+  V3 lo{FLT_MAX, FLT_MAX, FLT_MAX};
+  V3 hi{-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  void merge(const AABB& o) {
+    for (int i = 0; i < 3; ++i) { lo[i] = smin(lo[i], o.lo[i]); hi[i] = smax(hi[i], o.hi[i]); }
+  }
+  void merge(const V3& p) {
+    for (int i = 0; i < 3; ++i) { lo[i] = smin(lo[i], p[i]); hi[i] = smax(hi[i], p[i]); }
+  }
+  int longest_axis() const {
+    float x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+    if (x > y && x > z) return 0;
+    if (y > z) return 1;
+    return 2;
+  }
+  bool intersect(const Ray& r) const {  // shapes.cpp:55-72 (note the DOUBLE 1e-6 threshold)
+    float tn = std::numeric_limits<float>::lowest(), tf = std::numeric_limits<float>::max();
+    for (int i = 0; i < 3; ++i) {
+      if ((double)std::fabs(r.direction[i]) < 1e-6) {
+        if (r.origin[i] < lo[i] || r.origin[i] > hi[i]) return false;
+      } else {
+        float t1 = (lo[i] - r.origin[i]) / r.direction[i];
+        float t2 = (hi[i] - r.origin[i]) / r.direction[i];
+        if (t1 > t2) std::swap(t1, t2);
+        tn = smax(tn, t1);
+        tf = smin(tf, t2);
+        if (tn > tf || tf < 0) return false;
+      }
+    }
+    return true;
+  }
+};
+
+using M4 = std::array<std::array<float, 4>, 4>;
+
+struct Stats {
+  uint64_t rays = 0, box_tests = 0, prim_tests = 0;
+};
+
+struct Shape {
+  enum Kind { SPHERE, CUBE, RECTANGLE, PLANE } kind;
+  Material material;
+  V3 velocity{0, 0, 0};
+  M4 w2o{}, o2w{};
+  V3 corners[4];
+  int order = 0;
+  explicit Shape(Kind k) : kind(k) {}
+
+  static M4 mul(const M4& A, const M4& B) {  // shapes.cpp:140-148
+    M4 R{};
+    for (int i = 0; i < 4; i++)
+      for (int j = 0; j < 4; j++)
+        for (int k = 0; k < 4; k++) R[i][j] += A[i][k] * B[k][j];
+    return R;
+  }
+  void build(const V3& t, const V3& r, const V3& s) {  // shapes.cpp:92-138
+    M4 S = {{{s[0], 0, 0, 0}, {0, s[1], 0, 0}, {0, 0, s[2], 0}, {0, 0, 0, 1}}};
+    float cx = (float)std::cos((double)r[0]), sx = (float)std::sin((double)r[0]);
+    float cy = (float)std::cos((double)r[1]), sy = (float)std::sin((double)r[1]);
+    float cz = (float)std::cos((double)r[2]), sz = (float)std::sin((double)r[2]);
+    M4 R = {{{cy * cz, sx * sy * cz - cx * sz, cx * sy * cz + sx * sz, 0},
+             {cy * sz, sx * sy * sz + cx * cz, cx * sy * sz - sx * cz, 0},
+             {-sy, sx * cy, cx * cy, 0},
+             {0, 0, 0, 1}}};
+    M4 T = {{{1, 0, 0, t[0]}, {0, 1, 0, t[1]}, {0, 0, 1, t[2]}, {0, 0, 0, 1}}};
+    o2w = mul(T, mul(R, S));
+    M4 iS = {{{1.0f / s[0], 0, 0, 0}, {0, 1.0f / s[1], 0, 0}, {0, 0, 1.0f / s[2], 0}, {0, 0, 0, 1}}};
+    M4 iR = {{{R[0][0], R[1][0], R[2][0], 0}, {R[0][1], R[1][1], R[2][1], 0}, {R[0][2], R[1][2], R[2][2], 0}, {0, 0, 0, 1}}};
+    M4 iT = {{{1, 0, 0, -t[0]}, {0, 1, 0, -t[1]}, {0, 0, 1, -t[2]}, {0, 0, 0, 1}}};
+    w2o = mul(mul(iS, iR), iT);
+  }
+  static V3 xpoint(const M4& m, const V3& p) {  // shapes.cpp:151-158
+    V3 r;
+    float w = m[3][0] * p[0] + m[3][1] * p[1] + m[3][2] * p[2] + m[3][3];
+    for (int i = 0; i < 3; i++) r[i] = m[i][0] * p[0] + m[i][1] * p[1] + m[i][2] * p[2] + m[i][3];
+    if (std::fabs(w - 1.0f) > 1e-6f && w != 0) { r[0] /= w; r[1] /= w; r[2] /= w; }
+    return r;
+  }
+  static V3 xvec(const M4& m, const V3& v) {  // shapes.cpp:160-165
+    V3 r;
+    for (int i = 0; i < 3; i++) r[i] = m[i][0] * v[0] + m[i][1] * v[1] + m[i][2] * v[2];
+    return r;
+  }
+  V3 xnormal(const V3& n) const {  // shapes.cpp:167-187 (W2O transposed, renormalised)
+    V3 r;
+    r[0] = w2o[0][0] * n[0] + w2o[1][0] * n[1] + w2o[2][0] * n[2];
+    r[1] = w2o[0][1] * n[0] + w2o[1][1] * n[1] + w2o[2][1] * n[2];
+    r[2] = w2o[0][2] * n[0] + w2o[1][2] * n[1] + w2o[2][2] * n[2];
+    float len = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (len > 1e-6f) { r[0] /= len; r[1] /= len; r[2] /= len; }
+    return r;
+  }
+
+  AABB bbox() const {
+    AABB box;
+    switch (kind) {
+      case SPHERE: {  // shapes.cpp:264-287 (swept over time 0..1)
+        const float C[8][3] = {{-1, -1, -1}, {1, -1, -1}, {1, 1, -1}, {-1, 1, -1}, {-1, -1, 1}, {1, -1, 1}, {1, 1, 1}, {-1, 1, 1}};
+        for (auto& c : C) {
+          V3 p = xpoint(o2w, {c[0], c[1], c[2]});
+          box.merge(p);
+          box.merge(V3{p[0] + velocity[0], p[1] + velocity[1], p[2] + velocity[2]});
+        }
+        break;
+      }
+      case RECTANGLE: {  // shapes.cpp:335-343
+        const float C[4][3] = {{-0.5f, -0.5f, 0}, {0.5f, -0.5f, 0}, {0.5f, 0.5f, 0}, {-0.5f, 0.5f, 0}};
+        for (auto& c : C) box.merge(xpoint(o2w, {c[0], c[1], c[2]}));
+        break;
+      }
+      case CUBE: {  // shapes.cpp:425-433
+        const float C[8][3] = {{-0.5f, -0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {0.5f, 0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f},
+                               {-0.5f, -0.5f, 0.5f}, {0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, 0.5f}, {-0.5f, 0.5f, 0.5f}};
+        for (auto& c : C) box.merge(xpoint(o2w, {c[0], c[1], c[2]}));
+        break;
+      }
+      case PLANE: {  // shapes.cpp:496-503
+        const float pad = 1e-4f;
+        for (int i = 0; i < 4; ++i) box.merge(corners[i]);
+        for (int i = 0; i < 3; ++i) { box.lo[i] -= pad; box.hi[i] += pad; }
+        break;
+      }
+    }
+    return box;
+  }
+
+  bool intersect(Hit& hit, const Ray& ray) {
+    switch (kind) {
+      case SPHERE: return sphere(hit, ray);
+      case CUBE: return cube(hit, ray);
+      case RECTANGLE: return rect(hit, ray);
+      case PLANE: return plane(hit, ray);
+    }
+    return false;
+  }
+
+  bool sphere(Hit& hit, const Ray& ray) {  // shapes.cpp:200-262
+    Ray mv = ray;
+    mv.origin[0] -= velocity[0] * ray.time;
+    mv.origin[1] -= velocity[1] * ray.time;
+    mv.origin[2] -= velocity[2] * ray.time;
+    V3 o = xpoint(w2o, mv.origin), d = xvec(w2o, mv.direction);
+    float a = vdot(d, d);
+    float b = 2.0f * vdot(o, d);
+    float c = vdot(o, o) - 1.0f;
+    float disc = b * b - 4 * a * c;
+    if (disc < 0) return false;
+    float sq = std::sqrt(disc);
+    float t1 = (-b - sq) / (2.0f * a);
+    float t2 = (-b + sq) / (2.0f * a);
+    float tl = (t1 > 0.001f) ? t1 : ((t2 > 0.001f) ? t2 : -1.0f);
+    if (tl < 0) return false;
+    V3 pl = {o[0] + tl * d[0], o[1] + tl * d[1], o[2] + tl * d[2]};
+    V3 nl = pl;
+    hit.p = xpoint(o2w, pl);
+    hit.p[0] += velocity[0] * ray.time;
+    hit.p[1] += velocity[1] * ray.time;
+    hit.p[2] += velocity[2] * ray.time;
+    hit.n = xnormal(nl);
+    V3 dv = vsub(hit.p, ray.origin);
+    hit.t = std::sqrt(vdot(dv, dv));
+    hit.shape = this;
+    const float PI = 3.1415926535f;
+    hit.u = (float)(0.5f + std::atan2((double)nl[2], (double)nl[0]) / (double)(2.0f * PI));
+    hit.v = (float)(0.5f - std::asin((double)nl[1]) / (double)PI);
+    return true;
+  }
+
+  bool rect(Hit& hit, const Ray& ray) {  // shapes.cpp:299-333
+    V3 o = xpoint(w2o, ray.origin), d = xvec(w2o, ray.direction);
+    if (std::fabs(d[2]) < 1e-6f) return false;
+    float tl = -o[2] / d[2];
+    if (tl < 0.001f) return false;
+    float hx = o[0] + tl * d[0];
+    float hy = o[1] + tl * d[1];
+    if (hx < -0.5f || hx > 0.5f || hy < -0.5f || hy > 0.5f) return false;
+    hit.p = xpoint(o2w, {hx, hy, 0.0f});
+    hit.n = xnormal({0.0f, 0.0f, 1.0f});
+    V3 dv = vsub(hit.p, ray.origin);
+    hit.t = std::sqrt(vdot(dv, dv));
+    hit.shape = this;
+    hit.u = hx + 0.5f;
+    hit.v = hy + 0.5f;
+    return true;
+  }
+
+  bool cube(Hit& hit, const Ray& ray) {  // shapes.cpp:355-423
+    V3 o = xpoint(w2o, ray.origin), d = xvec(w2o, ray.direction);
+    const float tmin = -0.5f, tmax = 0.5f;
+    float tn = -std::numeric_limits<float>::max(), tf = std::numeric_limits<float>::max();
+    int axis = -1, sign = 0;
+    for (int i = 0; i < 3; i++) {
+      if (std::fabs(d[i]) < 1e-6f) {
+        if (o[i] < tmin || o[i] > tmax) return false;
+      } else {
+        float t1 = (tmin - o[i]) / d[i];
+        float t2 = (tmax - o[i]) / d[i];
+        float te = smin(t1, t2), tx = smax(t1, t2);
+        if (te > tn) { tn = te; axis = i; sign = (t1 < t2) ? -1 : 1; }
+        if (tx < tf) tf = tx;
+        if (tn > tf || tf < 0) return false;
+      }
+    }
+    float tl = (tn > 0) ? tn : tf;
+    if (tl < 0) return false;
+    V3 pl = {o[0] + tl * d[0], o[1] + tl * d[1], o[2] + tl * d[2]};
+    V3 nl = {0, 0, 0};
+    if (axis != -1) nl[axis] = (float)sign;
+    hit.p = xpoint(o2w, pl);
+    hit.n = xnormal(nl);
+    V3 dv = vsub(hit.p, ray.origin);
+    hit.t = std::sqrt(vdot(dv, dv));
+    hit.shape = this;
+    float uc = pl[0] + 0.5f, vc = pl[1] + 0.5f, wc = pl[2] + 0.5f;
+    if (axis == 0) { hit.u = (sign > 0) ? wc : (1.0f - wc); hit.v = vc; }
+    else if (axis == 1) { hit.u = uc; hit.v = (sign > 0) ? wc : (1.0f - wc); }
+    else { hit.u = (sign > 0) ? uc : (1.0f - uc); hit.v = vc; }
+    return true;
+  }
+
+  static bool in_tri(const V3& P, const V3& A, const V3& B, const V3& C, const V3& n) {  // shapes.cpp:24-40
+    if (vdot(vcross(vsub(B, A), vsub(P, A)), n) < -1e-6f) return false;
+    if (vdot(vcross(vsub(C, B), vsub(P, B)), n) < -1e-6f) return false;
+    if (vdot(vcross(vsub(A, C), vsub(P, C)), n) < -1e-6f) return false;
+    return true;
+  }
+  bool plane(Hit& hit, const Ray& ray) {  // shapes.cpp:444-494
+    V3 n = vcross(vsub(corners[1], corners[0]), vsub(corners[2], corners[0]));
+    float len = std::sqrt(vdot(n, n));
+    if (len < 1e-6f) return false;
+    n = {n[0] / len, n[1] / len, n[2] / len};
+    float denom = vdot(n, ray.direction);
+    if (std::fabs(denom) < 1e-6f) return false;
+    float t = vdot(vsub(corners[0], ray.origin), n) / denom;
+    if (t < 0) return false;
+    V3 P = {ray.origin[0] + t * ray.direction[0], ray.origin[1] + t * ray.direction[1], ray.origin[2] + t * ray.direction[2]};
+    // isPointInQuad recomputes the same normal (identical float ops)
+    V3 qn = vcross(vsub(corners[1], corners[0]), vsub(corners[2], corners[0]));
+    float l = std::sqrt(vdot(qn, qn));
+    qn[0] /= l; qn[1] /= l; qn[2] /= l;
+    if (!in_tri(P, corners[1], corners[3], corners[2], qn) && !in_tri(P, corners[0], corners[1], corners[2], qn)) return false;
+    V3 vu = vsub(corners[1], corners[0]), vv = vsub(corners[3], corners[0]), hv = vsub(P, corners[0]);
+    float u = vdot(hv, vu) / vdot(vu, vu);
+    float v = vdot(hv, vv) / vdot(vv, vv);
+    hit.u = smax(0.0f, smin(1.0f, u));
+    hit.v = smax(0.0f, smin(1.0f, v));
+    hit.p = P;
+    hit.n = n;
+    hit.t = t;
+    hit.shape = this;
+    return true;
+  }
+};
+
+// ---------------------------------------------------------------- BVH (acceleration.*)
+struct Node {
+  AABB box;
+  std::unique_ptr<Node> left, right;
+  std::vector<Shape*> objects;
+};
+
+struct BVH {
+  std::vector<Shape*> list;
+  Node root;
+  Stats* st = nullptr;
+  std::vector<Hit> tmp;
+  explicit BVH(const std::vector<Shape*>& shapes) : list(shapes) {  // acceleration.cpp:7-18
+    if (!list.empty()) build(0, (int)list.size(), root);
+    for (size_t i = 0; i < list.size(); ++i) list[i]->order = (int)i;
+  }
+  void build(int s, int e, Node& n) {  // acceleration.cpp:20-64
+    AABB box;
+    for (int i = s; i < e; i++) box.merge(list[i]->bbox());
+    n.box = box;
+    if (e - s <= 4) {
+      for (int i = s; i < e; i++) n.objects.push_back(list[i]);
+      return;
+    }
+    int axis = box.longest_axis();
+    auto cmp = [axis](Shape* a, Shape* b) {
+      AABB ba = a->bbox(), bb = b->bbox();
+      float ca = (ba.lo[axis] + ba.hi[axis]) / 2.0f;
+      float cb = (bb.lo[axis] + bb.hi[axis]) / 2.0f;
+      return ca < cb;
+    };
+    std::sort(list.begin() + s, list.begin() + e, cmp);
+    int mid = (s + e) / 2;
+    n.left = std::make_unique<Node>();
+    n.right = std::make_unique<Node>();
+    build(s, mid, *n.left);
+    build(mid, e, *n.right);
+  }
+  void helper(const Ray& r, Node& n) {  // acceleration.cpp:67-100
+    if (st) st->box_tests++;
+    if (!n.box.intersect(r)) return;
+    if (n.left || n.right) {
+      if (n.left) helper(r, *n.left);
+      if (n.right) helper(r, *n.right);
+    } else {
+      for (Shape* s : n.objects) {
+        Hit h;
+        if (st) st->prim_tests++;
+        if (s->intersect(h, r)) tmp.push_back(h);
+      }
+    }
+  }
+  Hit intersect_tree(const Ray& r) {  // acceleration.cpp:103-118
+    helper(r, root);
+    if (tmp.empty()) {
+      Hit miss;
+      miss.t = std::numeric_limits<float>::max();
+      miss.shape = nullptr;
+      return miss;
+    }
+    auto it = std::min_element(tmp.begin(), tmp.end(), [](const Hit& a, const Hit& b) { return a.t < b.t; });
+    Hit res = *it;
+    tmp.clear();
+    return res;
+  }
+  Hit intersect_linear(const Ray& r) {  // acceleration.cpp:124-139
+    Hit best;
+    best.t = std::numeric_limits<float>::max();
+    best.shape = nullptr;
+    for (Shape* s : list) {
+      Hit h;
+      if (st) st->prim_tests++;
+      if (s->intersect(h, r) && h.t < best.t) best = h;
+    }
+    return best;
+  }
+  Hit get(const Ray& r, bool use_bvh) {  // acceleration.cpp:142-150
+    if (st) st->rays++;
+    return use_bvh ? intersect_tree(r) : intersect_linear(r);
+  }
+};
+
+// ---------------------------------------------------------------- RNG
+enum RngMode { RNG_MT19937 = 0, RNG_COUNTER = 1 };
+
+// splitmix64 finaliser; the GPU kernel implements the identical stream (rt_kernels.hip).
+static inline uint64_t mix64(uint64_t z) {
+  z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27; z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+struct Rng {
+  RngMode mode;
+  std::mt19937 gen;
+  std::uniform_real_distribution<double> dist{0.0, 1.0};
+  uint64_t seed_key = 0, key = 0, ctr = 0;
+  Rng(RngMode m, uint64_t seed) : mode(m), gen((std::mt19937::result_type)seed) {
+    seed_key = mix64(seed + 0x9E3779B97F4A7C15ull);
+  }
+  void begin_sample(uint64_t pixel, uint64_t sample) {
+    if (mode != RNG_COUNTER) return;
+    uint64_t pk = mix64(seed_key ^ (pixel * 0xD1B54A32D192ED03ull));
+    key = mix64(pk + (sample + 1) * 0x9E3779B97F4A7C15ull);
+    ctr = 0;
+  }
+  // one dist(gen): generate_canonical<double,53> over two 32-bit words (libstdc++)
+  double next() {
+    if (mode == RNG_MT19937) return dist(gen);
+    uint64_t w = mix64(key + (++ctr) * 0xDA942042E4DD58B5ull);
+    double sum = (double)(uint32_t)w + (double)(uint32_t)(w >> 32) * 4294967296.0;
+    double ret = sum / 18446744073709551616.0;
+    if (ret >= 1.0) ret = std::nextafter(1.0, 0.0);
+    return ret;
+  }
+};
+
+// ---------------------------------------------------------------- Camera (camera.*)
+struct Camera {
+  int resx = 0, resy = 0;
+  float sw = 0, sh = 0, focal = 0, aperture = 0.0f, focus_dist = 10.0f;
+  V3 loc{0, 0, 0}, gaze{0, 0, 0}, up{0, 0, 0};
+
+  static V3 norm(const V3& v) {  // camera.cpp:60-68
+    float m = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (m == 0.0f) return {0.0f, 0.0f, 0.0f};
+    return {v[0] / m, v[1] / m, v[2] / m};
+  }
+  static V3 cross(const V3& a, const V3& b) {  // camera.cpp:70-87
+    return {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  }
+  void ray(float px, float py, Rng& rng, V3& o, V3& d) {  // camera.cpp:98-179
+    float nx = 1 - (px / (float)resx) * 2;
+    float ny = 1 - (py / (float)resy) * 2;
+    float nxr = nx * (sw / 2.0f), nyr = ny * (sh / 2.0f);
+    V3 z = norm(gaze);
+    V3 x = norm(cross(up, z));
+    V3 y = norm(cross(z, x));
+    V3 dw;  // M_C2W rows are (x[i], y[i], z[i], loc[i]); dir_camera = (nxr, nyr, focal, 0)
+    for (int i = 0; i < 3; i++) dw[i] = x[i] * nxr + y[i] * nyr + z[i] * focal;
+    dw = norm(dw);
+    if (aperture <= 0.0f) { o = loc; d = dw; return; }
+    V3 fp = {loc[0] + dw[0] * focus_dist, loc[1] + dw[1] * focus_dist, loc[2] + dw[2] * focus_dist};
+    float rx, ry;
+    for (;;) {  // random_in_unit_disk, camera.cpp:90-96
+      rx = (float)rng.next() * 2.0f - 1.0f;
+      ry = (float)rng.next() * 2.0f - 1.0f;
+      if (rx * rx + ry * ry < 1.0f) break;
+    }
+    float lr = aperture / 2.0f;
+    rx *= lr; ry *= lr;
+    V3 off = {x[0] * rx + y[0] * ry, x[1] * rx + y[1] * ry, x[2] * rx + y[2] * ry};
+    o = {loc[0] + off[0], loc[1] + off[1], loc[2] + off[2]};
+    d = norm(V3{fp[0] - o[0], fp[1] - o[1], fp[2] - o[2]});
+  }
+};
+
+// ---------------------------------------------------------------- scene loading
+struct Scene {
+  Camera cam;
+  std::vector<Light> lights;
+  std::vector<std::unique_ptr<Shape>> shapes;
+  std::unique_ptr<BVH> bvh;
+  std::string texture_root = "../../Textures/";
+};
+
+// json operator[] semantics used by camera.cpp:26-43: missing keys read as null
+static const oj::Value& jget(const oj::Value& v, const std::string& k) {
+  static const oj::Value null_v;
+  if (v.kind == oj::Value::Null) return null_v;
+  if (!v.is_object()) throw oj::error("type_error.305");
+  auto it = v.o.find(k);
+  return it == v.o.end() ? null_v : it->second;
+}
+static const oj::Value& jidx(const oj::Value& v, size_t i) {
+  static const oj::Value null_v;
+  if (v.kind == oj::Value::Null) return null_v;
+  if (!v.is_array()) throw oj::error("type_error.305");
+  return i < v.a.size() ? v.a[i] : null_v;
+}
+
+static Material parse_material(const oj::Value& m, const std::string& tex_root) {  // json_loader.cpp:30-97
+  Material mat;
+  try {
+    float tmp[3];
+    if (m.contains("diffuse_color")) { m.o.at("diffuse_color").get_vec3(tmp); mat.diffuse_color = {tmp[0], tmp[1], tmp[2]}; }
+    if (m.contains("specular_color")) { m.o.at("specular_color").get_vec3(tmp); mat.specular_color = {tmp[0], tmp[1], tmp[2]}; }
+    mat.k_ambient = m.value_float("k_ambient", 0.1f);
+    mat.k_diffuse = m.value_float("k_diffuse", 0.6f);
+    mat.k_specular = m.value_float("k_specular", 0.6f);
+    float rough = m.value_float("roughness", 0.001f);
+    rough = smax(0.001f, rough);
+    float r = smax(0.001f, smin(1.0f, rough));
+    mat.shininess = 5.0f / (r * r);
+    mat.roughness = m.value_float("roughness", 0.0f);
+    mat.reflectivity = m.value_float("reflectivity", 0.0f);
+    mat.transparency = m.value_float("transparency", 0.0f);
+    mat.refractive_index = m.value_float("refractive_index", 1.0f);
+    if (m.contains("texture_file") && !m.o.at("texture_file").empty()) {
+      std::string fn = m.o.at("texture_file").get_string();
+      if (!fn.empty()) {
+        std::string changed = std::string(fn.begin(), fn.end() - (fn.size() >= 3 ? 3 : fn.size())) + "ppm";
+        changed = tex_root + changed;
+        mat.texture = std::make_shared<Texture>(changed);
+        if (mat.texture->width == 0 || !mat.texture->loaded) {
+          std::cerr << "Warning: Failed to load texture file: " << changed << std::endl;
+          mat.texture = nullptr;
+        }
+      }
+    }
+  } catch (oj::error& e) {
+    std::cerr << "Warning: Error parsing material data: " << e.what() << std::endl;
+    return Material();
+  }
+  return mat;
+}
+
+static std::string slurp(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f.is_open()) throw std::runtime_error("Error: Could not open JSON file: " + path);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+static bool load_scene(const std::string& path, Scene& sc, int res_override_w, int res_override_h) {
+  std::string text = slurp(path);
+  oj::Value j;
+  try { j = oj::parse(text); } catch (oj::error& e) { throw std::runtime_error(std::string("Error: JSON parsing error: ") + e.what()); }
+  // Camera::readCameraSpec (camera.cpp:14-58): sequential reads, first failure keeps the rest default
+  Camera& c = sc.cam;
+  if (j.contains("cameras") && j.contains("render")) {
+    try {
+      const oj::Value& c0 = jidx(jget(j, "cameras"), 0);
+      c.focal = jget(c0, "focal_length").get_float();
+      c.aperture = c0.value_float("aperture", 0.0f);
+      c.focus_dist = c0.value_float("focus_dist", 10.0f);
+      jget(c0, "location").get_vec3(c.loc.data());
+      jget(c0, "gaze_vector").get_vec3(c.gaze.data());
+      jget(c0, "up_vector").get_vec3(c.up.data());
+      c.sw = (float)jget(c0, "sensor_width").get_int();
+      c.sh = (float)jget(c0, "sensor_height").get_int();
+      c.resx = jget(jget(j, "render"), "resolution_x").get_int();
+      c.resy = jget(jget(j, "render"), "resolution_y").get_int();
+    } catch (oj::error& e) {
+      std::cerr << "An unexpected error occurred: " << e.what() << std::endl;
+    }
+  } else {
+    std::cerr << "Error: JSON file is missing required keys." << std::endl;
+  }
+  if (res_override_w > 0 && res_override_h > 0) { c.resx = res_override_w; c.resy = res_override_h; }
+
+  // load_lights_from_json (json_loader.cpp:103-158)
+  if (j.contains("lights") && j.o.at("lights").is_array()) {
+    for (const auto& lj : j.o.at("lights").a) {
+      if (!lj.is_object()) { std::cerr << "Warning: Skipping non-object entry in 'lights' array." << std::endl; continue; }
+      try {
+        if (!lj.contains("location") || !lj.contains("color") || !lj.contains("intensity")) {
+          std::cerr << "Warning: Skipping invalid light definition." << std::endl;
+          continue;
+        }
+        Light L;
+        lj.o.at("location").get_vec3(L.location.data());
+        lj.o.at("color").get_vec3(L.color.data());
+        L.intensity = lj.o.at("intensity").get_float();
+        L.radius = lj.value_float("radius", 0.0f);
+        if (L.intensity <= 0) { std::cerr << "Warning: Skipping light with non-positive intensity." << std::endl; continue; }
+        sc.lights.push_back(L);
+      } catch (oj::error& e) {
+        std::cerr << "Warning: Error parsing light entry: " << e.what() << std::endl;
+      }
+    }
+  }
+
+  // load_shapes_from_json (json_loader.cpp:164-339): spheres, cubes, rectangles, planes
+  auto arr = [&](const char* k) -> const std::vector<oj::Value>* {
+    if (j.contains(k) && j.o.at(k).is_array()) return &j.o.at(k).a;
+    return nullptr;
+  };
+  if (auto* a = arr("spheres")) {
+    for (const auto& s : *a) {
+      if (!s.is_object()) continue;
+      try {
+        V3 t, r{0, 0, 0}, sc3{1, 1, 1}, vel{0, 0, 0};
+        jget(s, "location").get_vec3(t.data());
+        if (s.contains("rotation")) s.o.at("rotation").get_vec3(r.data());
+        if (s.contains("scale") && s.o.at("scale").is_array()) s.o.at("scale").get_vec3(sc3.data());
+        else if (s.contains("radius")) { float rr = s.o.at("radius").get_float(); sc3 = {rr, rr, rr}; }
+        Material mat;
+        if (s.contains("material")) mat = parse_material(s.o.at("material"), sc.texture_root);
+        if (s.contains("velocity")) s.o.at("velocity").get_vec3(vel.data());
+        vel[0] = vel[0] / 5; vel[1] = vel[1] / 5; vel[2] = vel[2] / 5;
+        auto sh = std::make_unique<Shape>(Shape::SPHERE);
+        sh->material = mat;
+        sh->velocity = vel;
+        sh->build(t, r, sc3);
+        sc.shapes.push_back(std::move(sh));
+      } catch (oj::error& e) { std::cerr << "Warning: Error parsing sphere: " << e.what() << std::endl; }
+    }
+  }
+  if (auto* a = arr("cubes")) {
+    for (const auto& s : *a) {
+      if (!s.is_object()) continue;
+      try {
+        if (!s.contains("translation") || !s.contains("rotation")) { std::cerr << "Warning: Skipping invalid cube definition." << std::endl; continue; }
+        V3 t, r, sc3{1, 1, 1};
+        s.o.at("translation").get_vec3(t.data());
+        s.o.at("rotation").get_vec3(r.data());
+        if (s.contains("scale")) {
+          const auto& sv = s.o.at("scale");
+          if (sv.is_array()) sv.get_vec3(sc3.data());
+          else if (sv.is_number()) { float x = sv.get_float(); sc3 = {x, x, x}; }
+        }
+        Material mat;
+        if (s.contains("material")) mat = parse_material(s.o.at("material"), sc.texture_root);
+        auto sh = std::make_unique<Shape>(Shape::CUBE);
+        sh->material = mat;
+        sh->build(t, r, sc3);
+        sc.shapes.push_back(std::move(sh));
+      } catch (oj::error& e) { std::cerr << "Warning: Error parsing cube entry: " << e.what() << std::endl; }
+    }
+  }
+  if (auto* a = arr("rectangles")) {
+    for (const auto& s : *a) {
+      if (!s.is_object()) continue;
+      try {
+        V3 t, r, sc3;
+        jget(s, "translation").get_vec3(t.data());
+        jget(s, "rotation").get_vec3(r.data());
+        jget(s, "scale").get_vec3(sc3.data());
+        Material mat;
+        if (s.contains("material")) mat = parse_material(s.o.at("material"), sc.texture_root);
+        auto sh = std::make_unique<Shape>(Shape::RECTANGLE);
+        sh->material = mat;
+        sh->build(t, r, sc3);
+        sc.shapes.push_back(std::move(sh));
+      } catch (oj::error& e) { std::cerr << "Warning: Error parsing rectangle: " << e.what() << std::endl; }
+    }
+  }
+  if (auto* a = arr("planes")) {
+    for (const auto& s : *a) {
+      if (!s.is_object()) continue;
+      try {
+        if (!s.contains("corners") || !s.o.at("corners").is_array() || s.o.at("corners").size() != 4) {
+          std::cerr << "Warning: Skipping invalid plane definition." << std::endl;
+          continue;
+        }
+        V3 cs[4];
+        for (size_t i = 0; i < 4; ++i) s.o.at("corners").a[i].get_vec3(cs[i].data());
+        Material mat;
+        if (s.contains("material")) mat = parse_material(s.o.at("material"), sc.texture_root);
+        auto sh = std::make_unique<Shape>(Shape::PLANE);
+        for (int i = 0; i < 4; ++i) sh->corners[i] = cs[i];
+        sh->material = mat;
+        sc.shapes.push_back(std::move(sh));
+      } catch (oj::error& e) { std::cerr << "Warning: Error parsing plane entry: " << e.what() << std::endl; }
+    }
+  }
+  std::vector<Shape*> ptrs;
+  for (auto& s : sc.shapes) ptrs.push_back(s.get());
+  sc.bvh = std::make_unique<BVH>(ptrs);
+  return true;
+}
+
+// ---------------------------------------------------------------- integrator (raytracer.cpp)
+static const int MAX_RECURSION_DEPTH = 10;  // raytracer.hpp:11
+
+static inline V3 normalize(const V3& v) {  // raytracer.cpp:75-79
+  float m = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+  if (m == 0.0f) return {0, 0, 0};
+  return {v[0] / m, v[1] / m, v[2] / m};
+}
+static inline V3 add(const V3& a, const V3& b) { return {a[0] + b[0], a[1] + b[1], a[2] + b[2]}; }
+static inline V3 mult(const V3& v, float s) { return {v[0] * s, v[1] * s, v[2] * s}; }
+
+static Ray reflect_ray(const Ray& ray, const Hit& h) {  // raytracer.cpp:101-115
+  float idn = vdot(ray.direction, h.n);
+  Ray r;
+  r.direction = vsub(ray.direction, mult(h.n, 2.0f * idn));
+  r.origin = add(h.p, mult(h.n, 1e-4f));
+  return r;
+}
+static Ray refract_ray(const Ray& ray, const Hit& h, float n_out) {  // raytracer.cpp:118-150
+  V3 I = ray.direction, N = h.n;
+  float n_in = 1.0f;
+  float cos_i = vdot(I, N);
+  if (cos_i > 0) { std::swap(n_in, n_out); N = mult(N, -1.0f); }
+  float eta = n_in / n_out;
+  float ca = std::fabs(cos_i);
+  float disc = 1.0f - eta * eta * (1.0f - ca * ca);
+  Ray r;
+  if (disc < 0) { r.origin = {0, 0, 0}; r.direction = {0, 0, 0}; return r; }
+  float cos_t = std::sqrt(disc);
+  V3 T = add(mult(I, eta), mult(N, (eta * ca - cos_t)));
+  r.origin = add(h.p, mult(N, -1e-4f));
+  r.direction = normalize(T);
+  return r;
+}
+static V3 random_in_unit_sphere(Rng& rng) {  // raytracer.cpp:153-171
+  for (;;) {
+    float r1 = (float)rng.next(), r2 = (float)rng.next(), r3 = (float)rng.next();
+    V3 p = {2.0f * r1 - 1.0f, 2.0f * r2 - 1.0f, 2.0f * r3 - 1.0f};
+    if (vdot(p, p) < 1.0f) return p;
+  }
+}
+
+struct Ctx {
+  Scene* sc;
+  bool use_bvh;
+  int light_samples;
+  Rng* rng;
+};
+
+static Color shade(const Hit& hit, const Ray& view, Ctx& cx) {  // raytracer.cpp:180-274
+  const Material& mat = hit.shape->material;
+  Color base = mat.diffuse(hit.u, hit.v);
+  Color fin = base * mat.k_ambient;
+  V3 V = normalize(vsub(view.origin, hit.p));
+  for (const Light& L : cx.sc->lights) {
+    float vis = 0.0f;
+    int ns = (L.radius > 0.0f) ? cx.light_samples : 1;
+    for (int s = 0; s < ns; ++s) {
+      V3 target = L.location;
+      if (L.radius > 0.0f) {
+        V3 off = random_in_unit_sphere(*cx.rng);
+        off = mult(off, L.radius);
+        target = add(target, off);
+      }
+      V3 lv = vsub(target, hit.p);
+      float ld = std::sqrt(vdot(lv, lv));
+      V3 Ls = normalize(lv);
+      Ray sr;
+      sr.origin = add(hit.p, mult(hit.n, 1e-4f));
+      sr.direction = Ls;
+      Hit sh = cx.sc->bvh->get(sr, cx.use_bvh);
+      if (!sh.shape || sh.t > ld) vis += 1.0f;
+    }
+    vis /= (float)ns;
+    if (vis <= 0.0f) continue;
+    V3 lc = vsub(L.location, hit.p);
+    float dsq = vdot(lc, lc);
+    float ldist = std::sqrt(dsq);
+    V3 Ld = normalize(lc);
+    float ndl = smax(0.0f, vdot(hit.n, Ld));
+    Color diff = base * ndl;
+    V3 H = normalize(add(Ld, V));
+    float ndh = smax(0.0f, vdot(hit.n, H));
+    float si = rt_powf(ndh, mat.shininess);
+    Color spec = mat.specular_color * si;
+    float att = 10.0f * L.intensity / (25.0f + 10.0f * ldist + 150.0f * dsq);
+    Color lcol = {L.color[0], L.color[1], L.color[2]};
+    Color contrib = lcol * (diff * mat.k_diffuse + spec * mat.k_specular) * att;
+    fin = fin + (contrib * vis);
+  }
+  return fin;
+}
+
+static Color trace(const Ray& ray, int depth, Ctx& cx) {  // raytracer.cpp:280-351
+  if (depth > MAX_RECURSION_DEPTH) return {0, 0, 0};
+  Hit hit = cx.sc->bvh->get(ray, cx.use_bvh);
+  if (!hit.shape) return {0.1f, 0.1f, 0.1f};
+  Color local = shade(hit, ray, cx);
+  const Material& mat = hit.shape->material;
+  Color refl = {0, 0, 0}, refr = {0, 0, 0};
+  if (mat.reflectivity > 0.0f) {
+    Ray rr = reflect_ray(ray, hit);
+    if (mat.roughness > 0.0f) {
+      V3 fuzz = random_in_unit_sphere(*cx.rng);
+      V3 pert = add(rr.direction, mult(fuzz, mat.roughness));
+      rr.direction = normalize(pert);
+      if (vdot(rr.direction, hit.n) < 0.0f) rr.direction = {0, 0, 0};
+    }
+    if (vdot(rr.direction, rr.direction) > 0.001f) refl = trace(rr, depth + 1, cx);
+  }
+  if (mat.transparency > 0.0f) {
+    Ray tr = refract_ray(ray, hit, mat.refractive_index);
+    if (vdot(tr.direction, tr.direction) > 1e-6f) refr = trace(tr, depth + 1, cx);
+  }
+  float lc = smax(0.0f, 1.0f - mat.reflectivity - mat.transparency);
+  return (lc * local) + (mat.reflectivity * refl) + (mat.transparency * refr);
+}
+
+static Color pixel_color(int x, int y, int s, Ctx& cx) {  // raytracer.cpp:18-70
+  Camera& cam = cx.sc->cam;
+  uint64_t pix = (uint64_t)y * (uint64_t)cam.resx + (uint64_t)x;
+  if (s <= 1) {
+    cx.rng->begin_sample(pix, 0);
+    Ray r;
+    cam.ray(x + 0.5f, y + 0.5f, *cx.rng, r.origin, r.direction);
+    r.time = (float)cx.rng->next();
+    return trace(r, 0, cx);
+  }
+  Color tot = {0, 0, 0};
+  int total = s * s;
+  for (int j = 0; j < s; ++j) {
+    for (int i = 0; i < s; ++i) {
+      cx.rng->begin_sample(pix, (uint64_t)(j * s + i));
+      double ox = cx.rng->next();
+      double oy = cx.rng->next();
+      double sx = (i + ox) / s;
+      double sy = (j + oy) / s;
+      Ray r;
+      cam.ray((float)(x + sx), (float)(y + sy), *cx.rng, r.origin, r.direction);
+      r.time = (float)cx.rng->next();
+      tot = tot + trace(r, 0, cx);
+    }
+  }
+  return tot / (float)total;
+}
+
+// raytracer.cpp:446-457 + image.cpp:28-37
+static inline int quantise(float c) {
+  float g = rt_powf(c, 1.0f / 1.1f);
+  int v = static_cast<int>(smax(0.0f, smin(1.0f, g)) * 255.999);
+  return std::max(0, std::min(v, 255));
+}
+
+}  // namespace orc
+
+// ---------------------------------------------------------------- C ABI (ctypes) + CLI
+extern "C" {
+
+struct oracle_params {
+  int use_bvh;         // -bvh
+  int spp_sqrt;        // -s
+  int light_samples;   // -light_sample
+  int rng_mode;        // 0 = mt19937 serial, 1 = counter
+  unsigned long long seed;
+  int res_w, res_h;    // 0 = from JSON
+  int x0, y0, w, h;    // region (counter mode); w=h=0 -> full image
+};
+struct oracle_stats {
+  unsigned long long rays, box_tests, prim_tests;
+  int width, height, n_shapes, n_lights;
+  double render_seconds, load_seconds;
+};
+
+// Renders a region into out_rgb (linear float RGB, pre-gamma, row-major region) and,
+// if out_u8 != NULL, the quantised 8-bit RGB of the same region.  Returns 0 on success.
+int oracle_render(const char* scene_path, const char* texture_root, const oracle_params* p,
+                  float* out_rgb, unsigned char* out_u8, oracle_stats* st) {
+  try {
+    auto t0 = std::chrono::steady_clock::now();
+    orc::Scene sc;
+    if (texture_root) sc.texture_root = texture_root;
+    orc::load_scene(scene_path, sc, p->res_w, p->res_h);
+    auto t1 = std::chrono::steady_clock::now();
+    int W = sc.cam.resx, H = sc.cam.resy;
+    int x0 = p->x0, y0 = p->y0, w = p->w ? p->w : W, h = p->h ? p->h : H;
+    if (W <= 0 || H <= 0) return -2;
+    if (p->rng_mode == orc::RNG_MT19937 && (x0 != 0 || y0 != 0 || w != W || h != H)) return -3;
+    orc::Stats stats;
+    sc.bvh->st = &stats;
+    orc::Rng rng((orc::RngMode)p->rng_mode, p->seed);
+    orc::Ctx cx{&sc, p->use_bvh != 0, p->light_samples, &rng};
+    for (int y = y0; y < y0 + h; ++y) {
+      for (int x = x0; x < x0 + w; ++x) {
+        orc::Color c = orc::pixel_color(x, y, p->spp_sqrt, cx);
+        size_t i = ((size_t)(y - y0) * w + (x - x0)) * 3;
+        if (out_rgb) { out_rgb[i] = c.r; out_rgb[i + 1] = c.g; out_rgb[i + 2] = c.b; }
+        if (out_u8) { out_u8[i] = (unsigned char)orc::quantise(c.r); out_u8[i + 1] = (unsigned char)orc::quantise(c.g); out_u8[i + 2] = (unsigned char)orc::quantise(c.b); }
+      }
+    }
+    auto t2 = std::chrono::steady_clock::now();
+    if (st) {
+      st->rays = stats.rays; st->box_tests = stats.box_tests; st->prim_tests = stats.prim_tests;
+      st->width = W; st->height = H; st->n_shapes = (int)sc.shapes.size(); st->n_lights = (int)sc.lights.size();
+      st->load_seconds = std::chrono::duration<double>(t1 - t0).count();
+      st->render_seconds = std::chrono::duration<double>(t2 - t1).count();
+    }
+    return 0;
+  } catch (std::exception& e) {
+    std::cerr << "oracle: " << e.what() << std::endl;
+    return -1;
+  }
+}
+
+// Scene metadata without rendering (resolution etc.); returns 0 on success.
+int oracle_scene_info(const char* scene_path, int* w, int* h, int* n_shapes, int* n_lights) {
+  try {
+    orc::Scene sc;
+    orc::load_scene(scene_path, sc, 0, 0);
+    *w = sc.cam.resx; *h = sc.cam.resy; *n_shapes = (int)sc.shapes.size(); *n_lights = (int)sc.lights.size();
+    return 0;
+  } catch (std::exception& e) {
+    std::cerr << "oracle: " << e.what() << std::endl;
+    return -1;
+  }
+}
+
+// Pure-function probes for unit tests (known-answer tests of the restated math).
+float oracle_powf(float x, float y) { return rt_powf(x, y); }
+int oracle_quantise(float c) { return orc::quantise(c); }
+double oracle_counter_draw(unsigned long long seed, unsigned long long pixel, unsigned long long sample, int n) {
+  orc::Rng r(orc::RNG_COUNTER, seed);
+  r.begin_sample(pixel, sample);
+  double v = 0;
+  for (int i = 0; i <= n; ++i) v = r.next();
+  return v;
+}
+
+}  // extern "C"
