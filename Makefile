@@ -1,0 +1,43 @@
+# Build of the MI355X ray-trace path (no cmake needed; outputs stay in-tree so they travel
+# to the GPU box with the snapshot).
+#   make            -> ray_tracying_amd/lib/librt_hip.so  (hipcc, gfx950 kernels + C ABI)
+#                      ray_tracying_amd/lib/librt_host.so (g++, scene loader / BVH / PPM)
+#                      ray_tracying_amd/bin/raytracer     (drop-in CLI)
+#                      oracle/liboracle.so, oracle/oracle_cli (CPU restatement, tests only)
+#   make ref        -> oracle/_ref/{Raytracer,ref_driver} from /root/reference (tests only)
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+# exact IEEE binary32: no FMA contraction, correctly rounded div/sqrt on the device
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fPIC -Wno-unused-result
+CXXFLAGS := -O2 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-function
+LIB := ray_tracying_amd/lib
+BIN := ray_tracying_amd/bin
+SRC := ray_tracying_amd/csrc
+COMMON_H := $(SRC)/common/rt_powf.h $(SRC)/common/glibc_powf_data.h include/rt_hip.h
+
+all: $(LIB)/librt_hip.so $(LIB)/librt_host.so $(BIN)/raytracer oracle
+
+$(LIB)/librt_hip.so: $(SRC)/hip/rt_hip.hip $(SRC)/hip/rt_device.h $(COMMON_H)
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) -shared $(SRC)/hip/rt_hip.hip -o $@
+
+HOST_SRC := $(SRC)/host/json_dom.cpp $(SRC)/host/scene.cpp $(SRC)/host/rt_host_api.cpp
+$(LIB)/librt_host.so: $(HOST_SRC) $(SRC)/host/json_dom.hpp $(SRC)/host/scene.hpp include/rt_host.h $(COMMON_H) $(LIB)/librt_hip.so
+	$(CXX) $(CXXFLAGS) -shared $(HOST_SRC) -o $@ -L$(LIB) -lrt_hip -Wl,-rpath,'$$ORIGIN'
+
+$(BIN)/raytracer: $(SRC)/host/main.cpp $(LIB)/librt_host.so
+	@mkdir -p $(BIN)
+	$(CXX) $(CXXFLAGS) $(SRC)/host/main.cpp -o $@ -L$(LIB) -lrt_host -lrt_hip -lpthread -Wl,-rpath,'$$ORIGIN/../lib'
+
+oracle:
+	$(MAKE) -C oracle all
+
+ref:
+	$(MAKE) -C oracle ref
+
+clean:
+	rm -rf $(LIB) $(BIN)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle ref clean

@@ -1,0 +1,189 @@
+/* rt_hip.h -- C ABI of the MI355X ray-trace hot path (librt_hip.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel path.  The reference has no
+ * FFI; its hot path is entered through C++ free functions and two internal seams, all of
+ * which this ABI replaces for a whole frame (or a list of image tiles) at a time:
+ *
+ *   rt_render_tiles()  replaces the y/x loop of main() calling
+ *                      compute_pixel_color(x, y, samples_sqrt, camera, bvh, lights,
+ *                      use_bvh, gen, dist, light_samples)
+ *                      (/root/reference/Code/raytracer.cpp:18-70, called at :433-476),
+ *                      and with it Trace (:280-351), shade (:180-274),
+ *                      BVH::get_intersection (/root/reference/Code/acceleration.cpp:142-150,
+ *                      acceleration.hpp:23) and Shapes::intersect (shapes.hpp:62).
+ *   rt_scene_create()  replaces BVH::BVH + the Shapes object graph as the thing traversal
+ *                      reads (acceleration.cpp:7-64, shapes.cpp:92-138): it takes the scene
+ *                      already flattened by the host (rt_host.h) into the records below.
+ *
+ * Conventions: plain pointers and sizes only; no C++ or torch types cross this ABI.
+ * Every function returns 0 on success or a negative RT_E* code; rt_last_error() returns a
+ * thread-local message for the last failure.  No C++ exception crosses the ABI.
+ * Host input descriptors are read during the call only (copied to device memory).
+ * Device output buffers are owned by the caller.
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_EINVAL -1   /* bad argument / descriptor */
+#define RT_EDEVICE -2  /* HIP runtime error (message in rt_last_error) */
+#define RT_ENOMEM -3   /* device allocation failed */
+#define RT_ENODEV -4   /* no HIP device / extension unusable */
+
+/* primitive kinds (tag bits 0..1) -- Sphere, Cube, Rectangle, Plane (shapes.hpp:89-140) */
+#define RT_PRIM_SPHERE 0
+#define RT_PRIM_CUBE 1
+#define RT_PRIM_RECTANGLE 2
+#define RT_PRIM_PLANE 3
+#define RT_TAG_KIND(tag) ((tag) & 3u)
+#define RT_TAG_PLANE_VALID 4u       /* Plane: |cross(c1-c0,c2-c0)| >= 1e-6f (shapes.cpp:450) */
+#define RT_TAG_MOVING 8u            /* Sphere with non-zero velocity (shapes.cpp:207-209) */
+#define RT_TAG_MATERIAL(tag) ((tag) >> 8)
+
+/* One primitive, 128 bytes (64-byte stride when every primitive is a Plane).
+ * Transformed kinds (Sphere/Cube/Rectangle):
+ *   a[0..11]  world_to_object rows 0..2 (m[i][0..3])      shapes.hpp:68
+ *   a[12..14] velocity (already /5, json_loader.cpp:221-223), a[15] = tag bits
+ *   b[0..11]  object_to_world rows 0..2                      shapes.hpp:69
+ * Plane (shapes.cpp:444-494; a triangle is a Plane with c3 == c0):
+ *   a[0..2]=c0 a[3]=n.x  a[4..6]=c1 a[7]=n.y  a[8..10]=c2 a[11]=n.z  a[12..14]=c3 a[15]=tag
+ *   n = normalize(cross(c1-c0, c2-c0)), computed on the host with the reference's ops.
+ * Records are stored in the reference's BVH-sorted order (acceleration.cpp:46-55): the
+ * record index is the tie-break order for equal hit distances. */
+typedef struct rt_prim {
+  float a[16];
+  float b[16];
+} rt_prim;
+
+/* BVH2 node, 64 bytes: the boxes of both children plus their references.
+ *   box[0..5]  = left  child lo.xyz, hi.xyz;  box[6..11] = right child lo.xyz, hi.xyz
+ *   ref > = 0 : internal child node index (its box is padded, tested conservatively)
+ *   cnt > 0   : leaf child; ref = first primitive, cnt = 1..4 primitives; its box is the
+ *               reference's exact leaf AABB and is tested with AABB::intersect semantics
+ *               (shapes.cpp:55-72) so the set of candidate primitives is the reference's.
+ *   ref == -1 && cnt == 0 : no child. */
+typedef struct rt_node {
+  float box[12];
+  int32_t ref_l, ref_r, cnt_l, cnt_r;
+} rt_node;
+
+/* Material (material.hpp:47-93 after json_loader.cpp:30-97), 64 bytes. */
+typedef struct rt_material {
+  float diffuse[3], k_ambient;
+  float specular[3], k_diffuse;
+  float k_specular, shininess, roughness, reflectivity;
+  float transparency, refractive_index;
+  int32_t texture; /* index into rt_scene_desc.textures or -1 */
+  int32_t pad;
+} rt_material;
+
+/* Point light (light.hpp:5-13), 32 bytes. */
+typedef struct rt_light {
+  float location[3], intensity;
+  float color[3], radius;
+} rt_light;
+
+/* P3 texture (image.hpp:8-11): width*height*3 bytes at texels + offset. */
+typedef struct rt_texture {
+  int32_t width, height;
+  int64_t offset;
+} rt_texture;
+
+typedef struct rt_scene_desc {
+  int32_t n_prims;
+  int32_t prim_stride; /* 64 (all planes) or 128 bytes */
+  const rt_prim* prims; /* n_prims records at prim_stride */
+  int32_t n_nodes;      /* 0 when n_prims == 0 */
+  int32_t tree_depth;   /* max root->leaf node count, sizes the LDS traversal stack */
+  const rt_node* nodes;
+  int32_t n_materials;
+  const rt_material* materials;
+  int32_t n_lights;
+  const rt_light* lights;
+  int32_t n_textures;
+  const rt_texture* textures;
+  int64_t n_texel_bytes;
+  const uint8_t* texels;
+  float scene_scale; /* max |coordinate| of scene bounds and camera, for pruning margins */
+  int32_t flags;     /* RT_SCENE_* feature bits (select kernel variants) */
+} rt_scene_desc;
+
+#define RT_SCENE_HAS_REFLECTION 1
+#define RT_SCENE_HAS_REFRACTION 2
+#define RT_SCENE_HAS_TEXTURE 4
+
+/* Camera after Camera::readCameraSpec (camera.cpp:14-58); the basis is precomputed on the
+ * host with the reference's own ops (camera.cpp:110-116): z = normalize(gaze),
+ * x = normalize(up x z), y = normalize(z x x); half_sensor = sensor/2.0f. */
+typedef struct rt_camera_desc {
+  int32_t res_x, res_y;
+  float half_sensor_w, half_sensor_h;
+  float location[3], focal_length;
+  float x_dir[3], aperture;
+  float y_dir[3], focus_dist;
+  float z_dir[3], pad;
+} rt_camera_desc;
+
+/* Render parameters: the reference's CLI flags (raytracer.cpp:361-390) + RNG key. */
+typedef struct rt_render_params {
+  int32_t spp_sqrt;      /* -s  (<=1: one ray through the pixel centre) */
+  int32_t light_samples; /* -light_sample */
+  int32_t use_bvh;       /* -bvh (0: linear search over all primitives, acceleration.cpp:124) */
+  int32_t count_work;    /* 1: instrumented kernel, fills box_tests / prim_tests */
+  uint64_t seed;         /* counter-RNG seed */
+  int32_t sync;          /* 1: synchronise and fill kernel_ms before returning */
+  int32_t pad;
+} rt_render_params;
+
+typedef struct rt_stats {
+  uint64_t rays;       /* BVH::get_intersection calls: camera + reflection + refraction + shadow */
+  uint64_t box_tests;  /* count_work only: AABB tests (32 B each in the roofline model) */
+  uint64_t prim_tests; /* count_work only: primitive tests (64 B each) */
+  double kernel_ms;    /* HIP-event time of the whole render (all logic+trace steps) */
+  double trace_ms;     /* HIP-event time summed over the trace_kernel launches only */
+  int32_t iterations;  /* logic->trace steps (== trace_kernel launches) */
+  int32_t pad;
+} rt_stats;
+
+typedef struct rt_scene_s* rt_scene_t;
+
+/* Number of visible HIP devices. */
+int rt_device_count(int32_t* count);
+
+/* Copy a flattened scene to `device` and return a handle that owns the device memory. */
+int rt_scene_create(int32_t device, const rt_scene_desc* desc, rt_scene_t* out);
+int rt_scene_destroy(rt_scene_t scene);
+
+/* Render the listed image tiles (tile id = ty * ceil(res_x/tile_w) + tx; tile_w, tile_h
+ * multiples of 8) into d_rgb_out, a DEVICE buffer of n_tiles*tile_w*tile_h*3 floats:
+ * tile k occupies [k*tile_w*tile_h*3, (k+1)*tile_w*tile_h*3), row-major RGB, linear
+ * (pre-gamma) colour == the reference's compute_pixel_color() result.  Pixels of a tile
+ * outside the image are left untouched.  `stream` is a hipStream_t (NULL = default).
+ * tile_ids is a HOST array. */
+int rt_render_tiles(rt_scene_t scene, const rt_camera_desc* cam, const rt_render_params* params,
+                    const int32_t* tile_ids, int32_t n_tiles, int32_t tile_w, int32_t tile_h,
+                    float* d_rgb_out, void* stream, rt_stats* stats);
+
+/* Small device-memory helpers so non-torch callers (ctypes tests, the C++ CLI) can drive
+ * rt_render_tiles without their own HIP runtime bindings. */
+int rt_malloc(int32_t device, size_t bytes, void** d_ptr);
+int rt_free(void* d_ptr);
+int rt_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
+int rt_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes);
+int rt_synchronize(int32_t device);
+
+/* Identification of the compiled device code (e.g. "gfx950"). */
+const char* rt_build_info(void);
+const char* rt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_HIP_H */

@@ -1,0 +1,946 @@
+// rt_hip.hip -- MI355X (gfx950) kernels + C ABI for the reference's per-pixel ray-trace path.
+//
+// Wavefront structure (two kernels per step, iterated until every pixel is done):
+//
+//   logic_kernel  one thread per SLOT (a pixel in flight).  Runs the reference's
+//                 compute_pixel_color -> Trace -> shade recursion as an explicit state
+//                 machine whose state lives in SoA HBM buffers between steps; consumes the
+//                 previous query's answer and advances until the slot needs the next scene
+//                 query, which it appends to a compact query list.  A slot renders all s*s
+//                 samples of its pixel in the reference's order (so the per-pixel sum is
+//                 evaluated in the reference's order), then pulls the next pixel from an
+//                 atomic counter.
+//   trace_kernel  one thread per query.  BVH::get_intersection (acceleration.cpp:142):
+//                 closest-hit for camera/reflection/refraction rays, any-hit-within-tmax for
+//                 shadow rays (== the reference's `!hit.shape || t > light_dist`,
+//                 raytracer.cpp:233).  BVH2 nodes (64 B = both child boxes), near-first
+//                 with t-pruning, per-lane stack in LDS (lane-minor -> conflict-free).
+//
+// Splitting them keeps the heavy recursion/shading state out of the traversal's registers
+// (fused, the allocator needed ~250 VGPRs = 1 wave/SIMD).  Leaf boxes are tested with the
+// reference's exact AABB::intersect (shapes.cpp:55-72) so the candidate set is the
+// reference's; internal boxes are padded on the host and tested by reciprocal slabs.
+// Ties on t resolve to the lowest primitive index == the reference's BVH-sorted order
+// (std::min_element, acceleration.cpp:112; strict < in intersect_linear, :133).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_device.h"
+
+using namespace rtd;
+
+namespace {
+
+constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------- slot state (SoA, HBM)
+// field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
+enum Field : int {
+  F_PIX = 0,   // launch-local pixel index, -1 = slot retired
+  F_SAMPLE,    // sample index within the pixel
+  F_CTRL,      // st | depth << 4
+  F_LIGHT,     // light index in shade
+  F_LS,        // shadow sample index for that light
+  F_RNG,       // draws consumed in the current sample
+  F_ACC,       // 3: per-pixel running sum (raytracer.cpp:63)
+  F_RAY = F_ACC + 3,  // 7: o, d, time of the Trace at `depth`
+  F_HP = F_RAY + 7,   // 3: hit point
+  F_HN = F_HP + 3,    // 3: hit normal
+  F_MAT = F_HN + 3,   // material of the hit
+  F_VIS,              // visibility accumulator of the current light
+  F_FIN = F_VIS + 1,  // 3: shade's final_color
+  F_UV = F_FIN + 3,   // 2: hit u, v (textures)
+  F_COUNT = F_UV + 2
+};
+// query record, one per slot: o(3) d(3); TMAX = light distance (shadow) or ray time
+// (closest); KIND bit 0 = shadow any-hit
+enum QField : int { Q_O = 0, Q_D = 3, Q_TMAX = 6, Q_KIND = 7, Q_COUNT = 8 };
+// frames for depths 0..kMaxDepth-1: A(3) + meta, and the pending refraction ray (6)
+enum FrField : int { FR_A = 0, FR_META = 3, FR_COUNT = 4 };
+
+enum : int { ST_SAMPLE = 0, ST_CLOSEST = 1, ST_SHADOW = 2 };
+
+struct Common {
+  const float4* prims;
+  int prim_stride4;
+  int n_prims;
+  const float4* nodes;
+  int use_bvh;
+  float eps_abs;
+};
+
+struct LogicArgs {
+  Common c;
+  const rt_material* mats;
+  const rt_light* lights;
+  int n_lights;
+  const rt_texture* textures;
+  const uint8_t* texels;
+  rt_camera_desc cam;
+  int spp_sqrt, light_samples;
+  uint64_t seed_key;
+  // work
+  const int* tile_ids;
+  int tile_w, tile_h, tiles_x, sub_x;
+  int n_pixels;  // n_tiles * tile_w * tile_h (launch-local pixel space)
+  unsigned int* next_pixel;
+  float* out;
+  // buffers
+  int n_slots;
+  uint32_t* state;
+  uint32_t* frames;      // [kMaxDepth][FR_COUNT][n_slots] (null if no reflection/refraction)
+  float* refr;           // [kMaxDepth][6][n_slots] (null if no refraction)
+  float* query;          // [Q_COUNT][n_slots]
+  const int* result;     // [n_slots]
+  int* qlist;            // compact list of slots with a pending query
+  unsigned int* qcount;
+};
+
+struct TraceArgs {
+  Common c;
+  const float* query;
+  int* result;
+  const int* qlist;
+  const unsigned int* qcount;
+  int n_slots;
+  int stack_depth;
+  unsigned long long* counters;  // box tests, prim tests (count_work)
+};
+
+// ---------------------------------------------------------------- traversal
+template <bool kCount>
+__device__ __forceinline__ void test_prims(const Common& a, int first, int cnt, const Ray& r, bool any,
+                                           float tmax, int& best_idx, float& best_t, bool& done,
+                                           unsigned int& nprim) {
+  for (int k = 0; k < cnt; ++k) {
+    int pi = first + k;
+    const float4* rec = a.prims + (size_t)pi * a.prim_stride4;
+    PrimA P;
+    load_prim_a(rec, P);
+    float t;
+    if (kCount) ++nprim;
+    if (prim_hit<false>(P, rec, r, t, nullptr)) {
+      if (any) {
+        if (!(t > tmax)) { done = true; return; }  // occludes: t <= light_dist
+      } else if (t < best_t || (t == best_t && pi < best_idx)) {
+        best_t = t;
+        best_idx = pi;
+      }
+    }
+  }
+}
+
+template <bool kCount>
+__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
+  extern __shared__ __attribute__((aligned(16))) int lds_stack[];
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const unsigned int nq = *ta.qcount;
+  unsigned int nbox = 0, nprim = 0;
+  if ((unsigned)i < nq) {
+    const Common& a = ta.c;
+    const int slot = ta.qlist[i];
+    const int N = ta.n_slots;
+    Ray r;
+    r.o = V3{ta.query[(Q_O + 0) * N + slot], ta.query[(Q_O + 1) * N + slot], ta.query[(Q_O + 2) * N + slot]};
+    r.d = V3{ta.query[(Q_D + 0) * N + slot], ta.query[(Q_D + 1) * N + slot], ta.query[(Q_D + 2) * N + slot]};
+    const float tq = ta.query[Q_TMAX * N + slot];
+    const int kind = __float_as_int(ta.query[Q_KIND * N + slot]);
+    const bool any = (kind & 1) != 0;
+    const float tmax = any ? tq : 0.0f;
+    r.time = any ? 0.0f : tq;  // shadow rays have time 0 (raytracer.cpp:225, shapes.hpp:28)
+    int best_idx = -1;
+    float best_t = __builtin_inff();
+    bool done = false;
+    if (a.n_prims > 0) {
+      if (!a.use_bvh) {  // BVH::intersect_linear (acceleration.cpp:124-139)
+        test_prims<kCount>(a, 0, a.n_prims, r, any, tmax, best_idx, best_t, done, nprim);
+      } else {
+        uint32_t par = 0;
+        par |= ((double)fabsf(r.d.x) < 1e-6) ? 1u : 0u;
+        par |= ((double)fabsf(r.d.y) < 1e-6) ? 2u : 0u;
+        par |= ((double)fabsf(r.d.z) < 1e-6) ? 4u : 0u;
+        auto safe_inv = [](float d) {
+          float dd = fabsf(d) < 1e-12f ? copysignf(1e-12f, d) : d;
+          return 1.0f / dd;
+        };
+        const V3 inv{safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z)};
+        int* stack = lds_stack + threadIdx.x;
+        int sp = 0, node = 0;
+        while (true) {
+          const float4* nd = a.nodes + (size_t)node * 4;
+          const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
+          const int4 nr = *reinterpret_cast<const int4*>(nd + 3);
+          const float bl_lo[3] = {n0.x, n0.y, n0.z}, bl_hi[3] = {n0.w, n1.x, n1.y};
+          const float br_lo[3] = {n1.z, n1.w, n2.x}, br_hi[3] = {n2.y, n2.z, n2.w};
+          float lim = any ? tmax : best_t;
+          lim = lim + (lim * 1e-5f + a.eps_abs);
+          bool hl = false, hr = false;
+          float tl = 0.f, tr = 0.f;
+          if (nr.z > 0) hl = aabb_exact(bl_lo, bl_hi, r, par, tl);
+          else if (nr.x >= 0) hl = aabb_fast(bl_lo, bl_hi, r.o, inv, tl);
+          if (nr.w > 0) hr = aabb_exact(br_lo, br_hi, r, par, tr);
+          else if (nr.y >= 0) hr = aabb_fast(br_lo, br_hi, r.o, inv, tr);
+          if (kCount) nbox += (nr.z > 0 || nr.x >= 0) + (nr.w > 0 || nr.y >= 0);
+          hl = hl && !(tl > lim);
+          hr = hr && !(tr > lim);
+          if (hl && nr.z > 0) {
+            test_prims<kCount>(a, nr.x, nr.z, r, any, tmax, best_idx, best_t, done, nprim);
+            hl = false;
+            if (done) break;
+          }
+          if (hr && nr.w > 0) {
+            test_prims<kCount>(a, nr.y, nr.w, r, any, tmax, best_idx, best_t, done, nprim);
+            hr = false;
+            if (done) break;
+          }
+          if (hl && hr) {
+            const bool lf = tl <= tr;
+            stack[sp * kBlock] = lf ? nr.y : nr.x;
+            ++sp;
+            node = lf ? nr.x : nr.y;
+          } else if (hl) {
+            node = nr.x;
+          } else if (hr) {
+            node = nr.y;
+          } else {
+            if (sp == 0) break;
+            --sp;
+            node = stack[sp * kBlock];
+          }
+        }
+      }
+    }
+    ta.result[slot] = any ? (done ? 1 : 0) : best_idx;
+  }
+  if (kCount) {
+    unsigned long long b = nbox, p = nprim;
+    for (int off = 32; off > 0; off >>= 1) {
+      b += __shfl_xor(b, off);
+      p += __shfl_xor(p, off);
+    }
+    if ((threadIdx.x & 63) == 0 && (b | p)) {
+      atomicAdd(ta.counters + 0, b);
+      atomicAdd(ta.counters + 1, p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- shading helpers
+// Material::getDiffuseColor (material.hpp:99-134)
+__device__ __forceinline__ V3 diffuse_color(const LogicArgs& a, const rt_material& m, float u, float v) {
+  V3 dc{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+  if (m.texture < 0) return dc;
+  rt_texture tx = a.textures[m.texture];
+  int x = (int)(u * (float)(tx.width - 1));
+  int y = (int)((1.0f - v) * (float)(tx.height - 1));
+  int cr = 0, cg = 0, cb = 0;
+  if (!(x < 0 || x >= tx.width || y < 0 || y >= tx.height)) {
+    const uint8_t* p = a.texels + tx.offset + ((size_t)y * tx.width + x) * 3;
+    cr = p[0]; cg = p[1]; cb = p[2];
+  }
+  V3 t{(((float)cr) / (255.0f)), (((float)cg) / (255.0f)), (((float)cb) / (255.0f))};
+  return V3{t.x * dc.x, t.y * dc.y, t.z * dc.z};
+}
+
+// Camera::pixelToRay_thin_lens (camera.cpp:98-179), basis precomputed on the host.
+__device__ __forceinline__ Ray camera_ray(const rt_camera_desc& c, float px, float py, Rng& rng) {
+  float nx = 1.0f - ((px) / ((float)c.res_x)) * 2.0f;
+  float ny = 1.0f - ((py) / ((float)c.res_y)) * 2.0f;
+  float nxr = nx * c.half_sensor_w, nyr = ny * c.half_sensor_h;
+  V3 dw{c.x_dir[0] * nxr + c.y_dir[0] * nyr + c.z_dir[0] * c.focal_length,
+        c.x_dir[1] * nxr + c.y_dir[1] * nyr + c.z_dir[1] * c.focal_length,
+        c.x_dir[2] * nxr + c.y_dir[2] * nyr + c.z_dir[2] * c.focal_length};
+  dw = normalize(dw);
+  Ray r;
+  r.time = 0.0f;
+  V3 loc{c.location[0], c.location[1], c.location[2]};
+  if (c.aperture <= 0.0f) {
+    r.o = loc;
+    r.d = dw;
+    return r;
+  }
+  V3 fp{loc.x + dw.x * c.focus_dist, loc.y + dw.y * c.focus_dist, loc.z + dw.z * c.focus_dist};
+  float rx, ry;
+  for (;;) {  // random_in_unit_disk (camera.cpp:90-96)
+    rx = (float)rng.next() * 2.0f - 1.0f;
+    ry = (float)rng.next() * 2.0f - 1.0f;
+    if (rx * rx + ry * ry < 1.0f) break;
+  }
+  float lr = c.aperture / 2.0f;
+  rx *= lr;
+  ry *= lr;
+  V3 off{c.x_dir[0] * rx + c.y_dir[0] * ry, c.x_dir[1] * rx + c.y_dir[1] * ry,
+         c.x_dir[2] * rx + c.y_dir[2] * ry};
+  r.o = add(loc, off);
+  r.d = normalize(sub(fp, r.o));
+  return r;
+}
+
+// launch-local pixel index -> image (x, y) and output offset; 8x8 blocks inside tiles so
+// consecutive slots trace spatially coherent rays.
+__device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, int& y, size_t& out_off) {
+  const int tile_px = a.tile_w * a.tile_h;
+  const int tl = p / tile_px, r = p - tl * tile_px;
+  const int b = r >> 6, l = r & 63;
+  const int lx = (b % a.sub_x) * 8 + (l & 7), ly = (b / a.sub_x) * 8 + (l >> 3);
+  const int tid = a.tile_ids[tl];
+  x = (tid % a.tiles_x) * a.tile_w + lx;
+  y = (tid / a.tiles_x) * a.tile_h + ly;
+  out_off = ((size_t)tl * tile_px + (size_t)ly * a.tile_w + lx) * 3;
+  return x < a.cam.res_x && y < a.cam.res_y;
+}
+
+// ---------------------------------------------------------------- logic kernel
+__global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
+  const int slot = blockIdx.x * kBlock + threadIdx.x;
+  bool want = false;
+  if (slot < a.n_slots) {
+    const int N = a.n_slots;
+    uint32_t* S = a.state;
+    auto ld = [&](int f) { return S[f * N + slot]; };
+    auto ldf = [&](int f) { return __uint_as_float(S[f * N + slot]); };
+    auto stu = [&](int f, uint32_t v) { S[f * N + slot] = v; };
+    auto stf = [&](int f, float v) { S[f * N + slot] = __float_as_uint(v); };
+
+    int pix = (int)ld(F_PIX);
+    if (pix >= 0) {
+      const int s = a.spp_sqrt;
+      const int total = s <= 1 ? 1 : s * s;
+      int sample = (int)ld(F_SAMPLE);
+      uint32_t ctrl = ld(F_CTRL);
+      int st = (int)(ctrl & 15u), depth = (int)(ctrl >> 4);
+      int light = (int)ld(F_LIGHT), ls = (int)ld(F_LS);
+      Rng rng;
+      rng.ctr = ld(F_RNG);
+      V3 acc{ldf(F_ACC), ldf(F_ACC + 1), ldf(F_ACC + 2)};
+      Ray ray;
+      ray.o = V3{ldf(F_RAY), ldf(F_RAY + 1), ldf(F_RAY + 2)};
+      ray.d = V3{ldf(F_RAY + 3), ldf(F_RAY + 4), ldf(F_RAY + 5)};
+      ray.time = ldf(F_RAY + 6);
+      V3 hp{ldf(F_HP), ldf(F_HP + 1), ldf(F_HP + 2)};
+      V3 hn{ldf(F_HN), ldf(F_HN + 1), ldf(F_HN + 2)};
+      int mat_id = (int)ld(F_MAT);
+      float vis = ldf(F_VIS);
+      V3 fin{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
+      float hu = ldf(F_UV), hv = ldf(F_UV + 1);
+      const int res = a.result[slot];
+      int px = 0, py = 0;
+      size_t out_off = 0;
+      bool inside = pixel_coords(a, pix, px, py, out_off);
+      uint64_t pixel_id = (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px;
+      rng.begin(a.seed_key, pixel_id, (uint64_t)sample);
+      rng.ctr = ld(F_RNG);
+      bool retired = false;
+      // query to emit
+      V3 qo{0, 0, 0}, qd{0, 0, 0};
+      float qtmax = 0.0f;
+      int qkind = 0;
+
+      while (!want && !retired) {
+        V3 ret{0, 0, 0};
+        bool returning = false;
+        bool shade_now = false;
+        if (st == ST_SAMPLE) {
+          if (sample >= total || !inside) {  // pixel finished: compute_pixel_color's average
+            if (inside) {
+              V3 c = (s <= 1) ? acc
+                              : V3{((acc.x) / ((float)total)), ((acc.y) / ((float)total)),
+                                   ((acc.z) / ((float)total))};
+              a.out[out_off] = c.x;
+              a.out[out_off + 1] = c.y;
+              a.out[out_off + 2] = c.z;
+            }
+            // pull the next in-image pixel
+            for (;;) {
+              unsigned int np = atomicAdd(a.next_pixel, 1u);
+              if ((int)np >= a.n_pixels) { retired = true; break; }
+              pix = (int)np;
+              if (pixel_coords(a, pix, px, py, out_off)) break;
+            }
+            inside = true;
+            if (retired) break;
+            pixel_id = (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px;
+            sample = 0;
+            acc = V3{0.0f, 0.0f, 0.0f};
+            continue;
+          }
+          // compute_pixel_color (raytracer.cpp:18-70): one sample
+          rng.begin(a.seed_key, pixel_id, (uint64_t)sample);
+          float fx, fy;
+          if (s <= 1) {
+            fx = (float)px + 0.5f;
+            fy = (float)py + 0.5f;
+          } else {
+            int si = sample % s, sj = sample / s;
+            double ox = rng.next();
+            double oy = rng.next();
+            double sx = ((double)si + ox) / (double)s;
+            double sy = ((double)sj + oy) / (double)s;
+            fx = (float)((double)px + sx);
+            fy = (float)((double)py + sy);
+          }
+          ray = camera_ray(a.cam, fx, fy, rng);
+          ray.time = (float)rng.next();
+          depth = 0;
+          st = ST_CLOSEST;
+          qo = ray.o;
+          qd = ray.d;
+          qtmax = ray.time;
+          qkind = 0;
+          want = true;
+          break;
+        }
+        if (st == ST_CLOSEST) {
+          // Trace body after get_intersection (raytracer.cpp:293-303)
+          if (res < 0) {
+            ret = V3{0.1f, 0.1f, 0.1f};
+            returning = true;
+          } else {
+            const float4* rec = a.c.prims + (size_t)res * a.c.prim_stride4;
+            PrimA P;
+            load_prim_a(rec, P);
+            HitAttr at;
+            float t;
+            prim_hit<true>(P, rec, ray, t, &at);  // bit-identical to the traversal's test
+            hp = at.p;
+            hn = at.n;
+            hu = at.u;
+            hv = at.v;
+            mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
+            const rt_material& m = a.mats[mat_id];
+            V3 base = diffuse_color(a, m, hu, hv);
+            fin = V3{base.x * m.k_ambient, base.y * m.k_ambient, base.z * m.k_ambient};
+            light = 0;
+            ls = 0;
+            vis = 0.0f;
+            shade_now = true;
+          }
+        } else if (st == ST_SHADOW) {
+          if (res == 0) vis += 1.0f;
+          ++ls;
+          shade_now = true;
+        }
+        if (shade_now) {  // shade (raytracer.cpp:180-274)
+          const rt_material& m = a.mats[mat_id];
+          while (light < a.n_lights) {
+            const rt_light& L = a.lights[light];
+            const int ns = (L.radius > 0.0f) ? a.light_samples : 1;
+            if (ls < ns) {
+              V3 target{L.location[0], L.location[1], L.location[2]};
+              if (L.radius > 0.0f) target = add(target, mul(rng.in_unit_sphere(), L.radius));
+              V3 lv = sub(target, hp);
+              qtmax = sqrtf(dot(lv, lv));
+              qd = normalize(lv);
+              qo = add(hp, mul(hn, 1e-4f));
+              qkind = 1;
+              st = ST_SHADOW;
+              want = true;
+              break;
+            }
+            vis = ((vis) / ((float)ns));
+            if (!(vis <= 0.0f)) {
+              V3 base = diffuse_color(a, m, hu, hv);
+              V3 V = normalize(sub(ray.o, hp));
+              V3 lc = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
+              float dsq = dot(lc, lc);
+              float ldist = sqrtf(dsq);
+              V3 Ld = normalize(lc);
+              float ndl = smax(0.0f, dot(hn, Ld));
+              V3 diff = mul(base, ndl);
+              V3 H = normalize(add(Ld, V));
+              float ndh = smax(0.0f, dot(hn, H));
+              float si = rt_powf(ndh, m.shininess);
+              V3 spec{m.specular[0] * si, m.specular[1] * si, m.specular[2] * si};
+              float att = ((10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq));
+              V3 inner{diff.x * m.k_diffuse + spec.x * m.k_specular, diff.y * m.k_diffuse + spec.y * m.k_specular,
+                       diff.z * m.k_diffuse + spec.z * m.k_specular};
+              V3 contrib{L.color[0] * inner.x * att, L.color[1] * inner.y * att, L.color[2] * inner.z * att};
+              fin = V3{fin.x + contrib.x * vis, fin.y + contrib.y * vis, fin.z + contrib.z * vis};
+            }
+            ++light;
+            ls = 0;
+            vis = 0.0f;
+          }
+          if (want) break;
+          // Trace continues with reflection / refraction (raytracer.cpp:303-350)
+          const float lcf = smax(0.0f, 1.0f - m.reflectivity - m.transparency);
+          const V3 A{lcf * fin.x, lcf * fin.y, lcf * fin.z};
+          bool refl_ok = false, refr_ok = false;
+          Ray rr, tr;
+          rr.time = 0.0f;
+          tr.time = 0.0f;
+          if (m.reflectivity > 0.0f) {  // createReflectionRay (raytracer.cpp:101-115) + glossy fuzz
+            float idn = dot(ray.d, hn);
+            rr.d = sub(ray.d, mul(hn, 2.0f * idn));
+            rr.o = add(hp, mul(hn, 1e-4f));
+            if (m.roughness > 0.0f) {
+              V3 fuzz = rng.in_unit_sphere();
+              rr.d = normalize(add(rr.d, mul(fuzz, m.roughness)));
+              if (dot(rr.d, hn) < 0.0f) rr.d = V3{0.0f, 0.0f, 0.0f};
+            }
+            refl_ok = dot(rr.d, rr.d) > 0.001f;
+          }
+          if (m.transparency > 0.0f) {  // createRefractionRay (raytracer.cpp:118-150)
+            V3 N = hn;
+            float n_in = 1.0f, n_out = m.refractive_index;
+            float cos_i = dot(ray.d, N);
+            if (cos_i > 0) {
+              float tmp = n_in;
+              n_in = n_out;
+              n_out = tmp;
+              N = mul(N, -1.0f);
+            }
+            float eta = ((n_in) / (n_out));
+            float ca = fabsf(cos_i);
+            float disc = 1.0f - eta * eta * (1.0f - ca * ca);
+            if (disc < 0) {
+              tr.o = V3{0, 0, 0};
+              tr.d = V3{0, 0, 0};
+            } else {
+              float cos_t = sqrtf(disc);
+              V3 T = add(mul(ray.d, eta), mul(N, (eta * ca - cos_t)));
+              tr.o = add(hp, mul(N, -1e-4f));
+              tr.d = normalize(T);
+            }
+            refr_ok = dot(tr.d, tr.d) > 1e-6f;
+          }
+          // a child that is not traced (invalid ray, or depth+1 > MAX) contributes (0,0,0)
+          const bool refl_go = refl_ok && depth + 1 <= kMaxDepth;
+          const bool refr_go = refr_ok && depth + 1 <= kMaxDepth;
+          if (!refl_go && !refr_go) {
+            V3 part{A.x + m.reflectivity * 0.0f, A.y + m.reflectivity * 0.0f, A.z + m.reflectivity * 0.0f};
+            ret = V3{part.x + m.transparency * 0.0f, part.y + m.transparency * 0.0f, part.z + m.transparency * 0.0f};
+            returning = true;
+          } else {
+            uint32_t* F = a.frames + (size_t)depth * FR_COUNT * N;
+            uint32_t meta = (uint32_t)mat_id << 2;
+            if (refl_go) {
+              F[(FR_A + 0) * N + slot] = __float_as_uint(A.x);
+              F[(FR_A + 1) * N + slot] = __float_as_uint(A.y);
+              F[(FR_A + 2) * N + slot] = __float_as_uint(A.z);
+              if (refr_go) {
+                meta |= 2;
+                float* R = a.refr + (size_t)depth * 6 * N;
+                R[0 * N + slot] = tr.o.x; R[1 * N + slot] = tr.o.y; R[2 * N + slot] = tr.o.z;
+                R[3 * N + slot] = tr.d.x; R[4 * N + slot] = tr.d.y; R[5 * N + slot] = tr.d.z;
+              }
+              ray = rr;
+            } else {  // reflection not traced: A + r*0, then straight into the refraction child
+              F[(FR_A + 0) * N + slot] = __float_as_uint(A.x + m.reflectivity * 0.0f);
+              F[(FR_A + 1) * N + slot] = __float_as_uint(A.y + m.reflectivity * 0.0f);
+              F[(FR_A + 2) * N + slot] = __float_as_uint(A.z + m.reflectivity * 0.0f);
+              meta |= 1;
+              ray = tr;
+            }
+            F[FR_META * N + slot] = meta;
+            ++depth;
+            st = ST_CLOSEST;
+            qo = ray.o;
+            qd = ray.d;
+            qtmax = 0.0f;  // secondary rays have time 0 (createReflectionRay returns {o, d})
+            qkind = 0;
+            want = true;
+            break;
+          }
+        }
+        // unwind finished Traces
+        while (returning) {
+          if (depth == 0) {
+            if (s <= 1) acc = ret;
+            else acc = V3{acc.x + ret.x, acc.y + ret.y, acc.z + ret.z};
+            ++sample;
+            st = ST_SAMPLE;
+            break;
+          }
+          --depth;
+          const uint32_t* F = a.frames + (size_t)depth * FR_COUNT * N;
+          uint32_t meta = F[FR_META * N + slot];
+          const rt_material& pm = a.mats[meta >> 2];
+          V3 A{__uint_as_float(F[(FR_A + 0) * N + slot]), __uint_as_float(F[(FR_A + 1) * N + slot]),
+               __uint_as_float(F[(FR_A + 2) * N + slot])};
+          if (!(meta & 1)) {  // the reflection child returned R
+            V3 p{A.x + pm.reflectivity * ret.x, A.y + pm.reflectivity * ret.y, A.z + pm.reflectivity * ret.z};
+            if (meta & 2) {  // refraction pending: trace it as the next child
+              uint32_t* Fw = a.frames + (size_t)depth * FR_COUNT * N;
+              Fw[(FR_A + 0) * N + slot] = __float_as_uint(p.x);
+              Fw[(FR_A + 1) * N + slot] = __float_as_uint(p.y);
+              Fw[(FR_A + 2) * N + slot] = __float_as_uint(p.z);
+              Fw[FR_META * N + slot] = meta | 1;
+              const float* R = a.refr + (size_t)depth * 6 * N;
+              ray.o = V3{R[0 * N + slot], R[1 * N + slot], R[2 * N + slot]};
+              ray.d = V3{R[3 * N + slot], R[4 * N + slot], R[5 * N + slot]};
+              ray.time = 0.0f;
+              ++depth;
+              st = ST_CLOSEST;
+              qo = ray.o;
+              qd = ray.d;
+              qtmax = 0.0f;
+              qkind = 0;
+              want = true;
+              break;
+            }
+            ret = V3{p.x + pm.transparency * 0.0f, p.y + pm.transparency * 0.0f, p.z + pm.transparency * 0.0f};
+          } else {  // the refraction child returned T
+            ret = V3{A.x + pm.transparency * ret.x, A.y + pm.transparency * ret.y, A.z + pm.transparency * ret.z};
+          }
+        }
+      }
+      if (retired) {
+        stu(F_PIX, 0xFFFFFFFFu);
+      } else {
+        stu(F_PIX, (uint32_t)pix);
+        stu(F_SAMPLE, (uint32_t)sample);
+        stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
+        stu(F_LIGHT, (uint32_t)light);
+        stu(F_LS, (uint32_t)ls);
+        stu(F_RNG, rng.ctr);
+        stf(F_ACC, acc.x); stf(F_ACC + 1, acc.y); stf(F_ACC + 2, acc.z);
+        stf(F_RAY, ray.o.x); stf(F_RAY + 1, ray.o.y); stf(F_RAY + 2, ray.o.z);
+        stf(F_RAY + 3, ray.d.x); stf(F_RAY + 4, ray.d.y); stf(F_RAY + 5, ray.d.z);
+        stf(F_RAY + 6, ray.time);
+        stf(F_HP, hp.x); stf(F_HP + 1, hp.y); stf(F_HP + 2, hp.z);
+        stf(F_HN, hn.x); stf(F_HN + 1, hn.y); stf(F_HN + 2, hn.z);
+        stu(F_MAT, (uint32_t)mat_id);
+        stf(F_VIS, vis);
+        stf(F_FIN, fin.x); stf(F_FIN + 1, fin.y); stf(F_FIN + 2, fin.z);
+        stf(F_UV, hu); stf(F_UV + 1, hv);
+        float* Q = a.query;
+        Q[(Q_O + 0) * N + slot] = qo.x; Q[(Q_O + 1) * N + slot] = qo.y; Q[(Q_O + 2) * N + slot] = qo.z;
+        Q[(Q_D + 0) * N + slot] = qd.x; Q[(Q_D + 1) * N + slot] = qd.y; Q[(Q_D + 2) * N + slot] = qd.z;
+        Q[Q_TMAX * N + slot] = qtmax;
+        Q[Q_KIND * N + slot] = __int_as_float(qkind);
+      }
+    }
+  }
+  // append slots with a query to the compact list: one atomic per wave
+  const unsigned long long m = __ballot(want);
+  if (m) {
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    unsigned int base = 0;
+    if (lane == leader) base = atomicAdd(a.qcount, (unsigned int)__popcll(m));
+    base = __shfl(base, leader);
+    if (want) a.qlist[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
+  }
+}
+
+// slot initialisation: slot k takes launch-local pixel k; a pixel outside the image (edge
+// tiles) is skipped by the first logic step, which pulls the next pixel instead.
+__global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, int* result) {
+  const int slot = blockIdx.x * kBlock + threadIdx.x;
+  if (slot >= n_slots) return;
+  for (int f = 0; f < F_COUNT; ++f) state[f * n_slots + slot] = 0u;
+  state[F_PIX * n_slots + slot] = (uint32_t)slot;
+  state[F_CTRL * n_slots + slot] = ST_SAMPLE;
+  result[slot] = -1;
+}
+
+// ---------------------------------------------------------------- C ABI support
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIP_TRY(expr, code)                                                                     \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return fail(code, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+uint64_t mix64_host(uint64_t z) {
+  z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27; z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+}  // namespace
+
+struct rt_scene_s {
+  int device = 0;
+  rt_scene_desc desc{};
+  void* d_prims = nullptr;
+  void* d_nodes = nullptr;
+  void* d_mats = nullptr;
+  void* d_lights = nullptr;
+  void* d_tex = nullptr;
+  void* d_texels = nullptr;
+  // per-render workspace (grown on demand)
+  void* d_ctl = nullptr;  // counters: [0] qcount, [1] next_pixel, [2..3] pad, [4..5] box/prim (u64)
+  int* d_tiles = nullptr;
+  size_t tiles_cap = 0;
+  uint32_t* d_state = nullptr;
+  uint32_t* d_frames = nullptr;
+  float* d_refr = nullptr;
+  float* d_query = nullptr;
+  int* d_result = nullptr;
+  int* d_qlist = nullptr;
+  size_t slots_cap = 0;
+  unsigned int* h_qcount = nullptr;  // pinned
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_a = nullptr, ev_b = nullptr;
+};
+
+static void free_workspace(rt_scene_s* s) {
+  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_qlist};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
+  s->d_query = nullptr; s->d_result = nullptr; s->d_qlist = nullptr;
+  s->slots_cap = 0;
+}
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+const char* rt_build_info(void) {
+  return "librt_hip: gfx950 hand-written HIP; wavefront logic+trace kernels; BVH2 + LDS stack; no MFMA";
+}
+
+int rt_device_count(int32_t* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(RT_ENODEV, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = n;
+  return RT_OK;
+}
+
+static int upload(void** dst, const void* src, size_t bytes) {
+  if (bytes == 0) {
+    *dst = nullptr;
+    return RT_OK;
+  }
+  HIP_TRY(hipMalloc(dst, bytes), RT_ENOMEM);
+  HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice), RT_EDEVICE);
+  return RT_OK;
+}
+
+int rt_scene_destroy(rt_scene_t s) {
+  if (!s) return RT_OK;
+  (void)hipSetDevice(s->device);
+  (void)hipDeviceSynchronize();
+  free_workspace(s);
+  void* ptrs[] = {s->d_prims, s->d_nodes, s->d_mats, s->d_lights, s->d_tex, s->d_texels, s->d_ctl, s->d_tiles};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (s->h_qcount) (void)hipHostFree(s->h_qcount);
+  hipEvent_t evs[] = {s->ev_t0, s->ev_t1, s->ev_a, s->ev_b};
+  for (hipEvent_t e : evs)
+    if (e) (void)hipEventDestroy(e);
+  delete s;
+  return RT_OK;
+}
+
+int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
+  if (!d || !out) return fail(RT_EINVAL, "rt_scene_create: null argument");
+  if (d->n_prims < 0 || (d->n_prims > 0 && (!d->prims || d->n_nodes <= 0 || !d->nodes)))
+    return fail(RT_EINVAL, "rt_scene_create: inconsistent primitive/node arrays");
+  if (d->prim_stride != 64 && d->prim_stride != 128)
+    return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
+  if (d->n_materials <= 0 || !d->materials) return fail(RT_EINVAL, "rt_scene_create: need >= 1 material");
+  if (d->n_lights < 0 || (d->n_lights > 0 && !d->lights)) return fail(RT_EINVAL, "rt_scene_create: bad lights");
+  if (d->tree_depth < 0 || d->tree_depth > 64) return fail(RT_EINVAL, "rt_scene_create: tree_depth out of range");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(RT_ENODEV, "rt_scene_create: no such HIP device");
+  HIP_TRY(hipSetDevice(device), RT_EDEVICE);
+  rt_scene_s* s = new rt_scene_s();
+  s->device = device;
+  s->desc = *d;
+  int rc = RT_OK;
+  if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
+      (rc = upload(&s->d_nodes, d->nodes, (size_t)d->n_nodes * sizeof(rt_node))) ||
+      (rc = upload(&s->d_mats, d->materials, (size_t)d->n_materials * sizeof(rt_material))) ||
+      (rc = upload(&s->d_lights, d->lights, (size_t)d->n_lights * sizeof(rt_light))) ||
+      (rc = upload(&s->d_tex, d->textures, (size_t)d->n_textures * sizeof(rt_texture))) ||
+      (rc = upload(&s->d_texels, d->texels, (size_t)d->n_texel_bytes))) {
+    rt_scene_destroy(s);
+    return rc;
+  }
+  if (hipMalloc(&s->d_ctl, 64) != hipSuccess || hipHostMalloc((void**)&s->h_qcount, 64) != hipSuccess ||
+      hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
+      hipEventCreate(&s->ev_a) != hipSuccess || hipEventCreate(&s->ev_b) != hipSuccess) {
+    rt_scene_destroy(s);
+    return fail(RT_ENOMEM, "rt_scene_create: control block / events");
+  }
+  s->desc.prims = nullptr; s->desc.nodes = nullptr; s->desc.materials = nullptr;
+  s->desc.lights = nullptr; s->desc.textures = nullptr; s->desc.texels = nullptr;
+  *out = s;
+  return RT_OK;
+}
+
+int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
+                    int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
+                    rt_stats* stats) {
+  if (!s || !cam || !p || (!tile_ids && n_tiles > 0) || !d_out) return fail(RT_EINVAL, "rt_render_tiles: null argument");
+  if (tile_w <= 0 || tile_h <= 0 || tile_w % 8 || tile_h % 8)
+    return fail(RT_EINVAL, "rt_render_tiles: tile size must be a positive multiple of 8");
+  if (cam->res_x <= 0 || cam->res_y <= 0) return fail(RT_EINVAL, "rt_render_tiles: camera resolution is 0");
+  if (p->spp_sqrt > 4096 || p->light_samples < 0) return fail(RT_EINVAL, "rt_render_tiles: bad sample counts");
+  const int tiles_x = (cam->res_x + tile_w - 1) / tile_w, tiles_y = (cam->res_y + tile_h - 1) / tile_h;
+  for (int i = 0; i < n_tiles; ++i)
+    if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(RT_EINVAL, "rt_render_tiles: tile id out of range");
+  if (stats) *stats = rt_stats{};
+  if (n_tiles == 0) return RT_OK;
+  const long long n_pixels_ll = (long long)n_tiles * tile_w * tile_h;
+  if (n_pixels_ll > 0x7fffffffLL) return fail(RT_EINVAL, "rt_render_tiles: too many pixels in one call");
+  const int n_pixels = (int)n_pixels_ll;
+  HIP_TRY(hipSetDevice(s->device), RT_EDEVICE);
+  hipStream_t stream = (hipStream_t)stream_ptr;
+
+  // ---- workspace
+  const bool need_frames = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
+  const bool need_refr = (s->desc.flags & RT_SCENE_HAS_REFRACTION) != 0;
+  const int n_slots = std::min(n_pixels, 1 << 20);
+  if ((size_t)n_tiles > s->tiles_cap) {
+    if (s->d_tiles) (void)hipFree(s->d_tiles);
+    s->d_tiles = nullptr;
+    s->tiles_cap = 0;
+    HIP_TRY(hipMalloc(&s->d_tiles, (size_t)n_tiles * sizeof(int32_t)), RT_ENOMEM);
+    s->tiles_cap = (size_t)n_tiles;
+  }
+  if ((size_t)n_slots > s->slots_cap || (need_frames && !s->d_frames) || (need_refr && !s->d_refr)) {
+    free_workspace(s);
+    size_t N = (size_t)std::max(n_slots, 1);
+    HIP_TRY(hipMalloc(&s->d_state, N * F_COUNT * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_qlist, N * 4), RT_ENOMEM);
+    if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
+    if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
+    s->slots_cap = N;
+  }
+  HIP_TRY(hipMemcpyAsync(s->d_tiles, tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream), RT_EDEVICE);
+  unsigned int* ctl = (unsigned int*)s->d_ctl;
+  HIP_TRY(hipMemsetAsync(ctl, 0, 64, stream), RT_EDEVICE);
+  unsigned int first_free = (unsigned int)n_slots;
+  HIP_TRY(hipMemcpyAsync(ctl + 1, &first_free, 4, hipMemcpyHostToDevice, stream), RT_EDEVICE);
+
+  LogicArgs la{};
+  Common c{};
+  c.prims = (const float4*)s->d_prims;
+  c.prim_stride4 = s->desc.prim_stride / 16;
+  c.n_prims = s->desc.n_prims;
+  c.nodes = (const float4*)s->d_nodes;
+  c.use_bvh = p->use_bvh;
+  c.eps_abs = 1e-5f * (s->desc.scene_scale > 1.0f ? s->desc.scene_scale : 1.0f);
+  la.c = c;
+  la.mats = (const rt_material*)s->d_mats;
+  la.lights = (const rt_light*)s->d_lights;
+  la.n_lights = s->desc.n_lights;
+  la.textures = (const rt_texture*)s->d_tex;
+  la.texels = (const uint8_t*)s->d_texels;
+  la.cam = *cam;
+  la.spp_sqrt = p->spp_sqrt;
+  la.light_samples = p->light_samples;
+  la.seed_key = mix64_host(p->seed + 0x9E3779B97F4A7C15ull);
+  la.tile_ids = s->d_tiles;
+  la.tile_w = tile_w;
+  la.tile_h = tile_h;
+  la.tiles_x = tiles_x;
+  la.sub_x = tile_w / 8;
+  la.n_pixels = n_pixels;
+  la.next_pixel = ctl + 1;
+  la.out = d_out;
+  la.n_slots = n_slots;
+  la.state = s->d_state;
+  la.frames = s->d_frames;
+  la.refr = s->d_refr;
+  la.query = s->d_query;
+  la.result = s->d_result;
+  la.qlist = s->d_qlist;
+  la.qcount = ctl;
+
+  TraceArgs ta{};
+  ta.c = c;
+  ta.query = s->d_query;
+  ta.result = s->d_result;
+  ta.qlist = s->d_qlist;
+  ta.qcount = ctl;
+  ta.n_slots = n_slots;
+  ta.stack_depth = s->desc.tree_depth + 2;
+  ta.counters = (unsigned long long*)(ctl + 4);
+  const size_t lds = (size_t)ta.stack_depth * kBlock * sizeof(int);
+
+  const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, s->d_result);
+  HIP_TRY(hipGetLastError(), RT_EDEVICE);
+
+  // ---- iterate logic -> trace until no slot issues a query
+  uint64_t rays = 0;
+  double trace_ms = 0.0;
+  int iters = 0;
+  HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
+  for (;;) {
+    HIP_TRY(hipMemsetAsync(ctl, 0, 4, stream), RT_EDEVICE);
+    hipLaunchKernelGGL(logic_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, la);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    HIP_TRY(hipMemcpyAsync(s->h_qcount, ctl, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
+    if (p->count_work)
+      hipLaunchKernelGGL(trace_kernel<true>, dim3(slot_blocks), dim3(kBlock), lds, stream, ta);
+    else
+      hipLaunchKernelGGL(trace_kernel<false>, dim3(slot_blocks), dim3(kBlock), lds, stream, ta);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
+    HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
+    unsigned int nq = *s->h_qcount;
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->ev_a, s->ev_b), RT_EDEVICE);
+    trace_ms += ms;
+    rays += nq;
+    ++iters;
+    if (nq == 0) break;
+  }
+  HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
+  HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
+  if (stats) {
+    unsigned long long cnt[2] = {0, 0};
+    HIP_TRY(hipMemcpy(cnt, ctl + 4, sizeof(cnt), hipMemcpyDeviceToHost), RT_EDEVICE);
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1), RT_EDEVICE);
+    stats->rays = rays;
+    stats->box_tests = cnt[0];
+    stats->prim_tests = cnt[1];
+    stats->kernel_ms = ms;
+    stats->trace_ms = trace_ms;
+    stats->iterations = iters;
+  }
+  return RT_OK;
+}
+
+int rt_malloc(int32_t device, size_t bytes, void** d_ptr) {
+  if (!d_ptr) return fail(RT_EINVAL, "rt_malloc: null");
+  HIP_TRY(hipSetDevice(device), RT_EDEVICE);
+  HIP_TRY(hipMalloc(d_ptr, bytes), RT_ENOMEM);
+  return RT_OK;
+}
+int rt_free(void* d_ptr) {
+  if (d_ptr) HIP_TRY(hipFree(d_ptr), RT_EDEVICE);
+  return RT_OK;
+}
+int rt_memcpy_d2h(void* h, const void* d, size_t bytes) {
+  HIP_TRY(hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost), RT_EDEVICE);
+  return RT_OK;
+}
+int rt_memcpy_h2d(void* d, const void* h, size_t bytes) {
+  HIP_TRY(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice), RT_EDEVICE);
+  return RT_OK;
+}
+int rt_synchronize(int32_t device) {
+  HIP_TRY(hipSetDevice(device), RT_EDEVICE);
+  HIP_TRY(hipDeviceSynchronize(), RT_EDEVICE);
+  return RT_OK;
+}
+
+}  // extern "C"

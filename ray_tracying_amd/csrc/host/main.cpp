@@ -1,0 +1,149 @@
+// main.cpp -- `raytracer`: drop-in replacement for the reference binary's CLI
+// (/root/reference/Code/raytracer.cpp:356-488) with the hot path on MI355X.
+//
+// Same flags and the same relative-path convention as the reference:
+//   -input NAME        scene at ../../ASCII/NAME        (raytracer.cpp:358,397)
+//   -output NAME       image at ../../Output/NAME        (default output.ppm, :365,398)
+//   -bvh               BVH traversal (default: linear search, :361)
+//   -s N               N x N stratified samples per pixel (default 4, :362)
+//   -light_sample N    shadow samples per area light (default 1, :363)
+// Additive flags (no reference counterpart):
+//   -scene PATH / -out PATH   scene / image paths used verbatim
+//   -res WxH           override render.resolution_x/y
+//   -seed N            counter-RNG seed (the reference seeds mt19937 from random_device)
+//   -device N          first HIP device;  -gpus N  split the image over N devices
+//   -textures DIR/     texture directory (default ../../Textures/)
+//   -float-out PATH    also dump the linear float RGB framebuffer (pre-gamma)
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/rt_hip.h"
+#include "../../../include/rt_host.h"
+
+int main(int argc, char* argv[]) {
+  std::string scene_file_path = "../../ASCII/";
+  bool use_bvh = false;
+  int n_samples_sqrt = 4;
+  int light_samples = 1;
+  std::string scene_file_name, output_file_name = "output.ppm";
+  std::string scene_verbatim, out_verbatim, float_out, textures = "../../Textures/";
+  int res_w = 0, res_h = 0, device = 0, gpus = 1;
+  unsigned long long seed = 20251226ull;
+  for (int i = 1; i < argc; ++i) {
+    if (std::strcmp(argv[i], "-bvh") == 0) use_bvh = true;
+    else if (std::strcmp(argv[i], "-s") == 0 && i + 1 < argc) n_samples_sqrt = std::atoi(argv[++i]);
+    else if (std::strcmp(argv[i], "-light_sample") == 0 && i + 1 < argc) light_samples = std::atoi(argv[++i]);
+    else if (std::strcmp(argv[i], "-input") == 0 && i + 1 < argc) scene_file_name = argv[++i];
+    else if (std::strcmp(argv[i], "-output") == 0 && i + 1 < argc) output_file_name = argv[++i];
+    else if (std::strcmp(argv[i], "-scene") == 0 && i + 1 < argc) scene_verbatim = argv[++i];
+    else if (std::strcmp(argv[i], "-out") == 0 && i + 1 < argc) out_verbatim = argv[++i];
+    else if (std::strcmp(argv[i], "-res") == 0 && i + 1 < argc) std::sscanf(argv[++i], "%dx%d", &res_w, &res_h);
+    else if (std::strcmp(argv[i], "-seed") == 0 && i + 1 < argc) seed = std::strtoull(argv[++i], nullptr, 10);
+    else if (std::strcmp(argv[i], "-device") == 0 && i + 1 < argc) device = std::atoi(argv[++i]);
+    else if (std::strcmp(argv[i], "-gpus") == 0 && i + 1 < argc) gpus = std::atoi(argv[++i]);
+    else if (std::strcmp(argv[i], "-textures") == 0 && i + 1 < argc) textures = argv[++i];
+    else if (std::strcmp(argv[i], "-float-out") == 0 && i + 1 < argc) float_out = argv[++i];
+  }
+  if (scene_file_name.empty() && scene_verbatim.empty()) {
+    std::cerr << "Error: Please specify scene file name" << std::endl;
+    std::cout << "Correct usage: ./Raytracer -name {scene_file_name.json}" << std::endl;
+    return 1;
+  }
+  const std::string scene_file = scene_verbatim.empty() ? scene_file_path + scene_file_name : scene_verbatim;
+  const std::string output_file = out_verbatim.empty() ? "../../Output/" + output_file_name : out_verbatim;
+
+  rth_scene_t scene = nullptr;
+  if (rth_scene_load(scene_file.c_str(), textures.c_str(), res_w, res_h, &scene) != 0) {
+    std::cerr << "An error occurred: " << rth_last_error() << std::endl;
+    return 1;
+  }
+  rth_scene_info info{};
+  rth_scene_get_info(scene, &info);
+  const int width = info.width, height = info.height;
+  if (width == 0 || height == 0) {
+    std::cerr << "Error: Camera resolution is 0. Check scene.json." << std::endl;
+    rth_scene_free(scene);
+    return 1;
+  }
+  if (info.n_shapes == 0) std::cerr << "Warning: No shapes loaded to render." << std::endl;
+  std::cout << "BVH built. Mode: " << (use_bvh ? "ON" : "OFF") << std::endl;
+  std::cout << "Rendering " << width << "x" << height << " with " << n_samples_sqrt << "x" << n_samples_sqrt
+            << " samples" << " and " << light_samples << " light sampling points ..." << std::endl;
+
+  rt_render_params p{};
+  p.spp_sqrt = n_samples_sqrt;
+  p.light_samples = light_samples;
+  p.use_bvh = use_bvh ? 1 : 0;
+  p.seed = seed;
+  p.sync = 1;
+  std::vector<float> rgb((size_t)width * height * 3, 0.0f);
+  auto t0 = std::chrono::steady_clock::now();
+  uint64_t rays = 0;
+  if (gpus <= 1) {
+    rt_stats st{};
+    if (rth_render(scene, device, &p, rgb.data(), &st) != 0) {
+      std::cerr << "An error occurred: " << rth_last_error() << std::endl;
+      rth_scene_free(scene);
+      return 1;
+    }
+    rays = st.rays;
+  } else {
+    // image-tile data parallelism: tile t goes to device (t mod gpus), one host thread each
+    rt_scene_desc desc{};
+    rt_camera_desc cam{};
+    rth_scene_desc(scene, &desc);
+    rth_scene_camera(scene, &cam);
+    const int T = 64, tx = (width + T - 1) / T, ty = (height + T - 1) / T;
+    std::vector<int> err(gpus, 0);
+    std::vector<uint64_t> nr(gpus, 0);
+    std::vector<std::thread> th;
+    for (int g = 0; g < gpus; ++g) {
+      th.emplace_back([&, g]() {
+        std::vector<int32_t> tiles;
+        for (int t = g; t < tx * ty; t += gpus) tiles.push_back(t);
+        rt_scene_t ds = nullptr;
+        if ((err[g] = rt_scene_create(device + g, &desc, &ds)) != 0) return;
+        size_t nv = tiles.size() * T * T * 3;
+        void* d_out = nullptr;
+        if ((err[g] = rt_malloc(device + g, nv * sizeof(float), &d_out)) != 0) { rt_scene_destroy(ds); return; }
+        rt_stats st{};
+        err[g] = rt_render_tiles(ds, &cam, &p, tiles.data(), (int32_t)tiles.size(), T, T, (float*)d_out, nullptr, &st);
+        std::vector<float> packed(nv);
+        if (!err[g]) err[g] = rt_memcpy_d2h(packed.data(), d_out, nv * sizeof(float));
+        if (!err[g]) rth_unpack_tiles(packed.data(), tiles.data(), (int32_t)tiles.size(), T, T, width, height, rgb.data());
+        nr[g] = st.rays;
+        rt_free(d_out);
+        rt_scene_destroy(ds);
+      });
+    }
+    for (auto& t : th) t.join();
+    for (int g = 0; g < gpus; ++g) {
+      if (err[g]) {
+        std::cerr << "An error occurred: device " << device + g << ": " << rt_last_error() << std::endl;
+        rth_scene_free(scene);
+        return 1;
+      }
+      rays += nr[g];
+    }
+  }
+  double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  for (int y = 100; y < height; y += 100) std::cout << "Progress: " << (100 * y / height) << "%\n";
+  std::cout << "Rendering complete.\n";
+  std::cerr << "[rt-mi355x] " << rays << " rays in " << secs << " s (" << rays / secs * 1e-6 << " Mrays/s)\n";
+  std::vector<uint8_t> u8(rgb.size());
+  rth_quantise(rgb.data(), (int64_t)rgb.size(), u8.data());
+  if (!float_out.empty()) {
+    std::ofstream f(float_out, std::ios::binary);
+    f.write((const char*)rgb.data(), (std::streamsize)(rgb.size() * sizeof(float)));
+  }
+  rth_write_ppm(output_file.c_str(), width, height, u8.data());
+  rth_scene_free(scene);
+  return 0;
+}

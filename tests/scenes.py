@@ -1,0 +1,141 @@
+"""Scene fixtures for the parity tests.
+
+* ``ascii(...)``      -- the reference's own input scene (/root/reference/ASCII/scene.json,
+  committed as data under tests/golden/scenes/ascii_scene.json: 140 cubes + 1 rectangle +
+  2 lights), with the edits the survey's known-answer tests use (SURVEY.md section 4:
+  K1 = roughness 0, K4 = primary-only).
+* ``features(...)``   -- a hand-written scene that exercises every primitive kind and every
+  feature of the hot path: mirror / glass (refraction + TIR) / glossy spheres, a moving
+  (motion-blurred) ellipsoid, rotated cubes (one with default material), a reflective
+  floor rectangle, a textured quad plane and two triangles (planes with c3 == c0), a hard
+  and a soft (radius > 0) light, optional thin-lens depth of field.
+* ``soup(...)``       -- a seeded triangle soup written as ``planes`` with c3 == c0.
+Scenes are plain dicts; ``write(scene, path)`` dumps JSON whose floats round-trip exactly.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import os
+import random
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ASCII_PATH = os.path.join(GOLDEN, "scenes", "ascii_scene.json")
+TEXTURES = os.path.join(GOLDEN, "textures") + os.sep
+
+
+def write(scene: dict, path: str) -> str:
+    with open(path, "w") as f:
+        json.dump(scene, f, indent=1)
+    return path
+
+
+def ascii(res=(64, 64), roughness=None, primary_only=False, texture=None) -> dict:
+    with open(ASCII_PATH) as f:
+        s = json.load(f)
+    s["render"] = {"resolution_x": res[0], "resolution_y": res[1]}
+    for k in ("cubes", "rectangles"):
+        for o in s.get(k, []):
+            m = o["material"]
+            if roughness is not None:
+                m["roughness"] = roughness
+            if primary_only:
+                m["reflectivity"] = 0.0
+                m["transparency"] = 0.0
+            if texture is not None:
+                m["texture_file"] = texture
+    if primary_only:
+        s["lights"] = []
+    return s
+
+
+def features(res=(64, 48), aperture=0.0, focus=6.0, soft_radius=0.5, texture="checker.jpg") -> dict:
+    def mat(**kw):
+        m = {"diffuse_color": [0.7, 0.7, 0.7], "specular_color": [1.0, 1.0, 1.0], "roughness": 0.2,
+             "k_ambient": 0.1, "k_diffuse": 0.6, "k_specular": 0.4, "reflectivity": 0.0,
+             "transparency": 0.0, "refractive_index": 1.0}
+        m.update(kw)
+        return m
+
+    return {
+        "cameras": [{"location": [0.3, -6.0, 2.2], "gaze_vector": [0.0, 1.0, -0.28],
+                     "up_vector": [0.0, 0.28, 1.0], "focal_length": 35.0, "sensor_width": 36.0,
+                     "sensor_height": 24.0, "aperture": aperture, "focus_dist": focus}],
+        "render": {"resolution_x": res[0], "resolution_y": res[1]},
+        "lights": [
+            {"location": [4.0, -4.0, 6.0], "intensity": 800.0, "color": [1.0, 0.9, 0.8], "radius": 0.0},
+            {"location": [-3.0, -2.0, 5.0], "intensity": 500.0, "color": [0.6, 0.7, 1.0], "radius": soft_radius},
+            {"location": [0.0, 0.0, 9.0], "intensity": -5.0, "color": [1, 1, 1]},   # skipped: intensity <= 0
+            {"location": [0.0, 0.0, 9.0], "color": [1, 1, 1]},                       # skipped: no intensity
+        ],
+        "spheres": [
+            {"location": [-1.3, 0.2, 0.85], "radius": 0.8,
+             "material": mat(diffuse_color=[0.9, 0.9, 0.95], reflectivity=0.85, roughness=0.0)},
+            {"location": [1.0, -0.6, 0.7], "radius": 0.7,
+             "material": mat(diffuse_color=[0.8, 1.0, 0.9], transparency=0.85, refractive_index=1.5,
+                             reflectivity=0.1, roughness=0.0)},
+            {"location": [0.1, 1.6, 0.6], "rotation": [0.3, 0.2, 0.1], "scale": [0.5, 0.7, 0.45],
+             "velocity": [1.5, 0.0, 0.5],
+             "material": mat(diffuse_color=[0.2, 0.4, 0.9], reflectivity=0.3, roughness=0.3)},
+            {"location": [-0.4, -1.8, 0.35], "radius": 0.35},                       # default Material()
+        ],
+        "cubes": [
+            {"translation": [2.3, 1.0, 0.6], "rotation": [0.4, 0.2, 0.7], "scale": [0.8, 0.6, 1.0],
+             "material": mat(diffuse_color=[0.9, 0.2, 0.1], roughness=0.5)},
+            {"translation": [-2.4, 1.4, 0.5], "rotation": [0.0, 0.0, 0.6], "scale": 0.9},
+            {"translation": [0.0, 0.0, 9.0]},                                        # skipped: no rotation
+        ],
+        "rectangles": [
+            {"translation": [0.0, 0.0, 0.0], "rotation": [0.0, 0.0, 0.0], "scale": [12.0, 12.0, 1.0],
+             "material": mat(diffuse_color=[0.6, 0.6, 0.55], reflectivity=0.25, roughness=0.05)},
+        ],
+        "planes": [
+            {"corners": [[-3.0, 3.0, 0.01], [-1.0, 3.0, 0.01], [-1.0, 3.0, 2.0], [-3.0, 3.0, 2.0]],
+             "material": mat(diffuse_color=[1.0, 1.0, 1.0], texture_file=texture)},
+            {"corners": [[1.4, 2.6, 0.02], [2.9, 2.2, 0.02], [2.0, 2.4, 1.9], [1.4, 2.6, 0.02]],
+             "material": mat(diffuse_color=[0.95, 0.8, 0.2], reflectivity=0.2)},
+            {"corners": [[-0.5, 2.8, 1.4], [0.6, 2.9, 1.6], [0.0, 3.0, 2.6], [-0.5, 2.8, 1.4]]},
+            {"corners": [[0, 0, 0], [1, 1, 1], [2, 2, 2]]},                          # skipped: 3 corners
+        ],
+    }
+
+
+def soup(n=200, seed=5, res=(48, 48), light=True) -> dict:
+    rnd = random.Random(seed)
+    s = n ** (-1.0 / 3.0)
+    planes = []
+    for _ in range(n):
+        c = [rnd.uniform(-1, 1) for _ in range(3)]
+        v = [[c[k] + rnd.uniform(-s, s) for k in range(3)] for _ in range(3)]
+        planes.append({"corners": [v[0], v[1], v[2], v[0]]})
+    return {
+        "cameras": [{"location": [0.0, -4.0, 0.0], "gaze_vector": [0.0, 1.0, 0.0], "up_vector": [0.0, 0.0, 1.0],
+                     "focal_length": 35.0, "sensor_width": 36.0, "sensor_height": 36.0}],
+        "render": {"resolution_x": res[0], "resolution_y": res[1]},
+        "lights": [{"location": [2.0, -3.0, 3.0], "intensity": 600.0, "color": [1.0, 1.0, 1.0], "radius": 0.0}]
+        if light else [],
+        "planes": planes,
+    }
+
+
+# name -> (scene builder, CLI-equivalent render args).  These are the golden-vector cases.
+def cases() -> dict:
+    return {
+        "ascii_k1_bvh": (lambda: ascii((64, 64), roughness=0.0), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
+        "ascii_glossy_bvh": (lambda: ascii((48, 48)), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
+        "ascii_glossy_s2_linear": (lambda: ascii((32, 32)), dict(use_bvh=False, spp_sqrt=2, light_samples=1)),
+        "ascii_primary": (lambda: ascii((64, 64), primary_only=True), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
+        "ascii_textured": (lambda: ascii((48, 48), texture="checker.jpg"), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
+        "features_s1": (lambda: features(), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
+        "features_s2_ls3": (lambda: features(), dict(use_bvh=True, spp_sqrt=2, light_samples=3)),
+        "features_linear": (lambda: features((40, 30)), dict(use_bvh=False, spp_sqrt=1, light_samples=2)),
+        "features_dof": (lambda: features(aperture=0.25, focus=5.5), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
+        "soup_s1": (lambda: soup(300, seed=11), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
+        "soup_s3": (lambda: soup(120, seed=3, res=(32, 32)), dict(use_bvh=True, spp_sqrt=3, light_samples=1)),
+        "soup_linear": (lambda: soup(80, seed=4, res=(32, 32)), dict(use_bvh=False, spp_sqrt=1, light_samples=1)),
+    }
+
+
+def materialise(name: str, directory: str) -> tuple[str, dict]:
+    builder, args = cases()[name]
+    return write(copy.deepcopy(builder()), os.path.join(directory, name + ".json")), dict(args)
