@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X ray-trace path.
+
+Metric (BASELINE.json): Mrays/sec (primary+secondary), 1024x1024 @ 100 spp; % HBM roofline.
+Workload (north_star / SURVEY.md 8(d) C5 at the headline resolution): synthetic 1M-triangle
+soup (planes with c3 == c0, splitmix64 seed 20251226), 1024x1024, -s 10 (100 jittered spp),
+-bvh, -light_sample 1.  A ray is one BVH::get_intersection call (camera + reflection +
+refraction + shadow rays), counted by the kernels.  One step = one full frame.
+
+N GPUs: one process per GPU (torch.distributed, RCCL); the frame's 64x64 tiles are dealt
+round-robin to the ranks (image-tile data parallelism, fixed total work -> "strong"
+scaling), each rank renders its tiles into a device buffer and rank 0 gathers the packed
+tiles over RCCL/xGMI inside the timed step.  value = all ranks' rays / max-over-ranks time.
+
+roofline: per-ray algorithmic bytes (32 B per AABB test + 64 B per primitive test, counted
+by an instrumented run of the same frame) x rays per trace launch / the trace kernel's
+average launch duration (HIP events on the launch stream, summed over the timed steps).
+cpu_baseline: the compiled reference (oracle/_ref/ref_driver; kind "reference") -- or the
+oracle restatement if the reference binary is absent (kind "port") -- on rank 0 at N=1,
+single-threaded, on a bounded row band of the same frame.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec (primary+secondary), 1024x1024 @100spp; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+NODE_BYTES, PRIM_BYTES = 32, 64  # BASELINE.md / SURVEY.md 8(d) algorithmic bytes
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--tris", type=int, default=1_000_000)
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--spp-sqrt", type=int, default=10)
+    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=20251226)
+    ap.add_argument("--scene", default=None, help="render this scene.json instead of the soup")
+    ap.add_argument("--cpu-rows", type=int, default=12, help="rows of the frame in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-traffic", default=None, help="JSON with per-launch HBM bytes from rocprofv3 --pmc")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene_path: str, args, rank: int):
+    """Reference CPU path on a bounded sample: a centred band of rows of the same frame."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    W = H = args.res
+    y0 = H // 2 - args.cpu_rows // 2
+    y1 = y0 + args.cpu_rows
+    if os.path.exists(ref):
+        cmd = [ref, "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt), "-light_sample", "1",
+               "-seed", "42", "-rows", str(y0), str(y1)]
+        kind = "reference"
+    else:
+        cmd = [os.path.join(ROOT, "oracle", "oracle_cli"), "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt),
+               "-light_sample", "1", "-rng", "counter", "-seed", str(args.seed), "-region", "0", str(y0), str(W),
+               str(y1 - y0)]
+        kind = "port"
+    if not os.path.exists(cmd[0]):
+        return None
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp")
+    wall = time.time() - t0
+    if r.returncode != 0:
+        log("cpu baseline failed:", r.stderr[-2000:])
+        return None
+    st = json.loads(r.stdout.strip().splitlines()[-1])
+    rays = st["rays"]
+    secs = st["render_seconds"]
+    return {
+        "value": rays / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": kind,
+        "sample": (f"rows {y0}-{y1 - 1} of the {W}x{H} frame at {args.spp_sqrt ** 2} spp "
+                   f"({W * (y1 - y0)} px, {rays} rays, render {secs:.1f} s single-threaded; "
+                   f"scene load + BVH build {st['load_seconds']:.1f} s excluded; wall {wall:.1f} s)"),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import ray_tracying_amd as rt
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = local_rank
+    torch.cuda.set_device(dev)
+
+    # ---- scene: every rank builds the identical scene locally (deterministic generator)
+    if args.scene:
+        scene_path = args.scene
+        workload = os.path.basename(args.scene)
+    else:
+        scene_path = f"/tmp/rt_bench_soup_{args.tris}_{args.res}_{rank}.json"
+        if not os.path.exists(scene_path):
+            rt.make_soup(scene_path, args.tris, seed=20251226, width=args.res, height=args.res)
+        workload = f"synthetic triangle soup, {args.tris} triangles (planes c3=c0), splitmix64 seed 20251226"
+    t0 = time.time()
+    scene = rt.Scene(scene_path, resolution=(args.res, args.res))
+    load_s = time.time() - t0
+    W, H = scene.width, scene.height
+    ds = rt.DeviceScene(scene, dev)
+    T = args.tile
+    tiles_x, tiles_y = (W + T - 1) // T, (H + T - 1) // T
+    all_tiles = np.arange(tiles_x * tiles_y, dtype=np.int32)
+    mine = all_tiles[all_tiles % world == rank]
+    per_rank = (len(all_tiles) + world - 1) // world
+    out = torch.zeros(per_rank * T * T * 3, dtype=torch.float32, device=f"cuda:{dev}")
+    gather_list = [torch.empty_like(out) for _ in range(world)] if (dist and rank == 0) else None
+    log(f"[rank {rank}] scene {W}x{H}, {scene.info.n_shapes} shapes, {scene.info.n_nodes} nodes, depth "
+        f"{scene.info.tree_depth}, load+build {load_s:.1f} s; {len(mine)} tiles on cuda:{dev}")
+
+    params = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=1, use_bvh=True, seed=args.seed)
+
+    def step(seed):
+        params.seed = seed
+        st = ds.render_tiles(mine, T, T, out.data_ptr(), params)
+        if dist:
+            dist.gather(out, gather_list, dst=0)
+        return st
+
+    # ---- instrumented frame: algorithmic bytes per ray (same seed as the first timed step)
+    cp = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=1, use_bvh=True, seed=args.seed, count_work=True)
+    cst = ds.render_tiles(mine, T, T, out.data_ptr(), cp)
+    bytes_per_ray = (NODE_BYTES * cst.box_tests + PRIM_BYTES * cst.prim_tests) / max(cst.rays, 1)
+    log(f"[rank {rank}] instrumented: rays {cst.rays}, box tests {cst.box_tests} ({cst.box_tests / max(cst.rays, 1):.1f}/ray),"
+        f" prim tests {cst.prim_tests} ({cst.prim_tests / max(cst.rays, 1):.1f}/ray), {bytes_per_ray:.0f} B/ray")
+
+    for w in range(args.warmup):
+        step(args.seed + 1000 + w)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rays = 0
+    trace_ms = 0.0
+    launches = 0
+    for k in range(args.steps):
+        st = step(args.seed + k)
+        rays += st.rays
+        trace_ms += st.trace_ms
+        launches += st.iterations
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    tot = torch.tensor([float(rays), trace_ms, float(launches), bytes_per_ray * rays], dtype=torch.float64,
+                       device=f"cuda:{dev}")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+    if dist:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    rays_all, trace_ms_all, launches_all, alg_bytes_all = tot.tolist()
+    elapsed = tmax.item()
+
+    if rank == 0 and dist:  # sanity: the gathered framebuffer covers every tile with finite values
+        packed = torch.stack(gather_list).cpu().numpy()
+        assert np.isfinite(packed).all()
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    value = rays_all / elapsed / 1e6
+    # average trace-kernel launch: bytes it moves algorithmically / its duration (per-rank
+    # launches run concurrently on different GPUs, so average per launch, then x1 GPU)
+    avg_launch_ms = trace_ms_all / max(launches_all, 1)
+    avg_launch_bytes = alg_bytes_all / max(launches_all, 1)
+    achieved = avg_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
+    traffic = None
+    if args.pmc_traffic and os.path.exists(args.pmc_traffic):
+        traffic = json.load(open(args.pmc_traffic)).get("hbm_bytes_per_launch")
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(scene_path, args, rank)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": workload,
+            "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample 1",
+            "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}",
+            "rng": "counter (splitmix64 per pixel/sample)",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
+            "alg_bytes_per_ray": round(bytes_per_ray, 1), "launches_per_step": int(launches_all / args.steps),
+            "trace_share_of_step": round(trace_ms_all / world / (elapsed * 1e3), 3),
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -2,14 +2,16 @@
 //
 // Wavefront structure (two kernels per step, iterated until every pixel is done):
 //
-//   logic_kernel  one thread per SLOT (a pixel in flight).  Runs the reference's
-//                 compute_pixel_color -> Trace -> shade recursion as an explicit state
+//   logic_kernel  one thread per SLOT (one sample of one pixel in flight).  Runs the
+//                 reference's Trace -> shade recursion for that sample as an explicit state
 //                 machine whose state lives in SoA HBM buffers between steps; consumes the
 //                 previous query's answer and advances until the slot needs the next scene
-//                 query, which it appends to a compact query list.  A slot renders all s*s
-//                 samples of its pixel in the reference's order (so the per-pixel sum is
-//                 evaluated in the reference's order), then pulls the next pixel from an
-//                 atomic counter.
+//                 query, which it appends to a compact query list.  A finished sample writes
+//                 its colour to the sample buffer and the slot pulls the next (pixel, sample)
+//                 unit from an atomic counter (64 consecutive units = 64 samples of one pixel:
+//                 maximally coherent rays per wave).
+//   reduce_kernel one thread per pixel: compute_pixel_color's sum over the s*s samples in
+//                 the reference's order, then the division (raytracer.cpp:46-69).
 //   trace_kernel  one thread per query.  BVH::get_intersection (acceleration.cpp:142):
 //                 closest-hit for camera/reflection/refraction rays, any-hit-within-tmax for
 //                 shadow rays (== the reference's `!hit.shape || t > light_dist`,
@@ -42,14 +44,12 @@ constexpr int kBlock = 256;
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
 enum Field : int {
-  F_PIX = 0,   // launch-local pixel index, -1 = slot retired
-  F_SAMPLE,    // sample index within the pixel
+  F_UNIT = 0,  // work unit = launch-local pixel * n_samples + sample; -1 = slot retired
   F_CTRL,      // st | depth << 4
   F_LIGHT,     // light index in shade
   F_LS,        // shadow sample index for that light
   F_RNG,       // draws consumed in the current sample
-  F_ACC,       // 3: per-pixel running sum (raytracer.cpp:63)
-  F_RAY = F_ACC + 3,  // 7: o, d, time of the Trace at `depth`
+  F_RAY,       // 7: o, d, time of the Trace at `depth`
   F_HP = F_RAY + 7,   // 3: hit point
   F_HN = F_HP + 3,    // 3: hit normal
   F_MAT = F_HN + 3,   // material of the hit
@@ -89,7 +89,10 @@ struct LogicArgs {
   const int* tile_ids;
   int tile_w, tile_h, tiles_x, sub_x;
   int n_pixels;  // n_tiles * tile_w * tile_h (launch-local pixel space)
-  unsigned int* next_pixel;
+  int n_samples; // s*s (1 when s <= 1)
+  long long n_units;  // n_pixels * n_samples
+  unsigned long long* next_unit;
+  float* samples;  // [n_units][3] per-sample Trace colours
   float* out;
   // buffers
   int n_slots;
@@ -297,6 +300,14 @@ __device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, 
 }
 
 // ---------------------------------------------------------------- logic kernel
+// unit -> (launch-local pixel, sample); false if the pixel lies outside the image
+__device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, int& px, int& py, int& sample) {
+  const int p = (int)(unit / a.n_samples);
+  sample = (int)(unit - (long long)p * a.n_samples);
+  size_t off;
+  return pixel_coords(a, p, px, py, off);
+}
+
 __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
   bool want = false;
@@ -308,17 +319,12 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
     auto stu = [&](int f, uint32_t v) { S[f * N + slot] = v; };
     auto stf = [&](int f, float v) { S[f * N + slot] = __float_as_uint(v); };
 
-    int pix = (int)ld(F_PIX);
-    if (pix >= 0) {
+    long long unit = (long long)(int)ld(F_UNIT);
+    if (unit >= 0) {
       const int s = a.spp_sqrt;
-      const int total = s <= 1 ? 1 : s * s;
-      int sample = (int)ld(F_SAMPLE);
       uint32_t ctrl = ld(F_CTRL);
       int st = (int)(ctrl & 15u), depth = (int)(ctrl >> 4);
       int light = (int)ld(F_LIGHT), ls = (int)ld(F_LS);
-      Rng rng;
-      rng.ctr = ld(F_RNG);
-      V3 acc{ldf(F_ACC), ldf(F_ACC + 1), ldf(F_ACC + 2)};
       Ray ray;
       ray.o = V3{ldf(F_RAY), ldf(F_RAY + 1), ldf(F_RAY + 2)};
       ray.d = V3{ldf(F_RAY + 3), ldf(F_RAY + 4), ldf(F_RAY + 5)};
@@ -330,14 +336,12 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
       V3 fin{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
       float hu = ldf(F_UV), hv = ldf(F_UV + 1);
       const int res = a.result[slot];
-      int px = 0, py = 0;
-      size_t out_off = 0;
-      bool inside = pixel_coords(a, pix, px, py, out_off);
-      uint64_t pixel_id = (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px;
-      rng.begin(a.seed_key, pixel_id, (uint64_t)sample);
+      int px = 0, py = 0, sample = 0;
+      bool inside = unit_coords(a, unit, px, py, sample);
+      Rng rng;
+      rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
       rng.ctr = ld(F_RNG);
       bool retired = false;
-      // query to emit
       V3 qo{0, 0, 0}, qd{0, 0, 0};
       float qtmax = 0.0f;
       int qkind = 0;
@@ -347,31 +351,18 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
         bool returning = false;
         bool shade_now = false;
         if (st == ST_SAMPLE) {
-          if (sample >= total || !inside) {  // pixel finished: compute_pixel_color's average
-            if (inside) {
-              V3 c = (s <= 1) ? acc
-                              : V3{((acc.x) / ((float)total)), ((acc.y) / ((float)total)),
-                                   ((acc.z) / ((float)total))};
-              a.out[out_off] = c.x;
-              a.out[out_off + 1] = c.y;
-              a.out[out_off + 2] = c.z;
-            }
-            // pull the next in-image pixel
+          if (!inside) {  // edge tile: skip units outside the image
             for (;;) {
-              unsigned int np = atomicAdd(a.next_pixel, 1u);
-              if ((int)np >= a.n_pixels) { retired = true; break; }
-              pix = (int)np;
-              if (pixel_coords(a, pix, px, py, out_off)) break;
+              unsigned long long nu = atomicAdd(a.next_unit, 1ull);
+              if ((long long)nu >= a.n_units) { retired = true; break; }
+              unit = (long long)nu;
+              if (unit_coords(a, unit, px, py, sample)) break;
             }
-            inside = true;
             if (retired) break;
-            pixel_id = (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px;
-            sample = 0;
-            acc = V3{0.0f, 0.0f, 0.0f};
-            continue;
+            inside = true;
           }
-          // compute_pixel_color (raytracer.cpp:18-70): one sample
-          rng.begin(a.seed_key, pixel_id, (uint64_t)sample);
+          // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)
+          rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
           float fx, fy;
           if (s <= 1) {
             fx = (float)px + 0.5f;
@@ -396,8 +387,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
           want = true;
           break;
         }
-        if (st == ST_CLOSEST) {
-          // Trace body after get_intersection (raytracer.cpp:293-303)
+        if (st == ST_CLOSEST) {  // Trace body after get_intersection (raytracer.cpp:293-303)
           if (res < 0) {
             ret = V3{0.1f, 0.1f, 0.1f};
             returning = true;
@@ -443,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
               want = true;
               break;
             }
-            vis = ((vis) / ((float)ns));
+            vis = vis / (float)ns;
             if (!(vis <= 0.0f)) {
               V3 base = diffuse_color(a, m, hu, hv);
               V3 V = normalize(sub(ray.o, hp));
@@ -457,7 +447,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
               float ndh = smax(0.0f, dot(hn, H));
               float si = rt_powf(ndh, m.shininess);
               V3 spec{m.specular[0] * si, m.specular[1] * si, m.specular[2] * si};
-              float att = ((10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq));
+              float att = (10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq);
               V3 inner{diff.x * m.k_diffuse + spec.x * m.k_specular, diff.y * m.k_diffuse + spec.y * m.k_specular,
                        diff.z * m.k_diffuse + spec.z * m.k_specular};
               V3 contrib{L.color[0] * inner.x * att, L.color[1] * inner.y * att, L.color[2] * inner.z * att};
@@ -496,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
               n_out = tmp;
               N = mul(N, -1.0f);
             }
-            float eta = ((n_in) / (n_out));
+            float eta = n_in / n_out;
             float ca = fabsf(cos_i);
             float disc = 1.0f - eta * eta * (1.0f - ca * ca);
             if (disc < 0) {
@@ -551,11 +541,18 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
         }
         // unwind finished Traces
         while (returning) {
-          if (depth == 0) {
-            if (s <= 1) acc = ret;
-            else acc = V3{acc.x + ret.x, acc.y + ret.y, acc.z + ret.z};
-            ++sample;
-            st = ST_SAMPLE;
+          if (depth == 0) {  // the sample's Trace returned: store it, pull the next unit
+            a.samples[unit * 3 + 0] = ret.x;
+            a.samples[unit * 3 + 1] = ret.y;
+            a.samples[unit * 3 + 2] = ret.z;
+            unsigned long long nu = atomicAdd(a.next_unit, 1ull);
+            if ((long long)nu >= a.n_units) {
+              retired = true;
+            } else {
+              unit = (long long)nu;
+              inside = unit_coords(a, unit, px, py, sample);
+              st = ST_SAMPLE;
+            }
             break;
           }
           --depth;
@@ -592,15 +589,13 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
         }
       }
       if (retired) {
-        stu(F_PIX, 0xFFFFFFFFu);
+        stu(F_UNIT, 0xFFFFFFFFu);
       } else {
-        stu(F_PIX, (uint32_t)pix);
-        stu(F_SAMPLE, (uint32_t)sample);
+        stu(F_UNIT, (uint32_t)unit);
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
         stu(F_LIGHT, (uint32_t)light);
         stu(F_LS, (uint32_t)ls);
         stu(F_RNG, rng.ctr);
-        stf(F_ACC, acc.x); stf(F_ACC + 1, acc.y); stf(F_ACC + 2, acc.z);
         stf(F_RAY, ray.o.x); stf(F_RAY + 1, ray.o.y); stf(F_RAY + 2, ray.o.z);
         stf(F_RAY + 3, ray.d.x); stf(F_RAY + 4, ray.d.y); stf(F_RAY + 5, ray.d.z);
         stf(F_RAY + 6, ray.time);
@@ -630,13 +625,37 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
   }
 }
 
-// slot initialisation: slot k takes launch-local pixel k; a pixel outside the image (edge
-// tiles) is skipped by the first logic step, which pulls the next pixel instead.
-__global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, int* result) {
+// compute_pixel_color's accumulation (raytracer.cpp:46-69): totalColor starts at {0,0,0},
+// adds every sample's Trace colour in (j, i) order, then divides by (float)(s*s); with
+// s <= 1 the single Trace colour is returned as is.
+__global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
+  const int p = blockIdx.x * kBlock + threadIdx.x;
+  if (p >= a.n_pixels) return;
+  int x, y;
+  size_t off;
+  if (!pixel_coords(a, p, x, y, off)) return;
+  const float* smp = a.samples + (size_t)p * a.n_samples * 3;
+  V3 c;
+  if (a.spp_sqrt <= 1) {
+    c = V3{smp[0], smp[1], smp[2]};
+  } else {
+    V3 acc{0.0f, 0.0f, 0.0f};
+    for (int k = 0; k < a.n_samples; ++k) acc = V3{acc.x + smp[3 * k], acc.y + smp[3 * k + 1], acc.z + smp[3 * k + 2]};
+    const float tot = (float)a.n_samples;
+    c = V3{acc.x / tot, acc.y / tot, acc.z / tot};
+  }
+  a.out[off] = c.x;
+  a.out[off + 1] = c.y;
+  a.out[off + 2] = c.z;
+}
+
+// slot initialisation: slot k takes unit k (units past the end retire immediately); a unit
+// whose pixel is outside the image (edge tiles) is skipped by the first logic step.
+__global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, long long n_units, int* result) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
   if (slot >= n_slots) return;
   for (int f = 0; f < F_COUNT; ++f) state[f * n_slots + slot] = 0u;
-  state[F_PIX * n_slots + slot] = (uint32_t)slot;
+  state[F_UNIT * n_slots + slot] = (long long)slot < n_units ? (uint32_t)slot : 0xFFFFFFFFu;
   state[F_CTRL * n_slots + slot] = ST_SAMPLE;
   result[slot] = -1;
 }
@@ -673,27 +692,31 @@ struct rt_scene_s {
   void* d_tex = nullptr;
   void* d_texels = nullptr;
   // per-render workspace (grown on demand)
-  void* d_ctl = nullptr;  // counters: [0] qcount, [1] next_pixel, [2..3] pad, [4..5] box/prim (u64)
+  void* d_ctl = nullptr;  // bytes 0: qcount (u32), 8: next_unit (u64), 16/24: box/prim tests (u64)
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
   uint32_t* d_state = nullptr;
   uint32_t* d_frames = nullptr;
   float* d_refr = nullptr;
   float* d_query = nullptr;
+  float* d_samples = nullptr;
+  size_t samples_cap = 0;
   int* d_result = nullptr;
   int* d_qlist = nullptr;
   size_t slots_cap = 0;
   unsigned int* h_qcount = nullptr;  // pinned
+  unsigned long long h_ctl_init = 0;
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_a = nullptr, ev_b = nullptr;
 };
 
 static void free_workspace(rt_scene_s* s) {
-  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_qlist};
+  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_qlist, s->d_samples};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
-  s->d_query = nullptr; s->d_result = nullptr; s->d_qlist = nullptr;
+  s->d_query = nullptr; s->d_result = nullptr; s->d_qlist = nullptr; s->d_samples = nullptr;
   s->slots_cap = 0;
+  s->samples_cap = 0;
 }
 
 extern "C" {
@@ -801,7 +824,9 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // ---- workspace
   const bool need_frames = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
   const bool need_refr = (s->desc.flags & RT_SCENE_HAS_REFRACTION) != 0;
-  const int n_slots = std::min(n_pixels, 1 << 20);
+  const int n_samples = p->spp_sqrt <= 1 ? 1 : p->spp_sqrt * p->spp_sqrt;
+  const long long n_units = (long long)n_pixels * n_samples;
+  const int n_slots = (int)std::min<long long>(n_units, 1 << 20);
   if ((size_t)n_tiles > s->tiles_cap) {
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     s->d_tiles = nullptr;
@@ -820,11 +845,18 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
     s->slots_cap = N;
   }
+  if ((size_t)n_units * 3 > s->samples_cap) {
+    if (s->d_samples) (void)hipFree(s->d_samples);
+    s->d_samples = nullptr;
+    s->samples_cap = 0;
+    HIP_TRY(hipMalloc(&s->d_samples, (size_t)n_units * 3 * sizeof(float)), RT_ENOMEM);
+    s->samples_cap = (size_t)n_units * 3;
+  }
   HIP_TRY(hipMemcpyAsync(s->d_tiles, tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream), RT_EDEVICE);
   unsigned int* ctl = (unsigned int*)s->d_ctl;
   HIP_TRY(hipMemsetAsync(ctl, 0, 64, stream), RT_EDEVICE);
-  unsigned int first_free = (unsigned int)n_slots;
-  HIP_TRY(hipMemcpyAsync(ctl + 1, &first_free, 4, hipMemcpyHostToDevice, stream), RT_EDEVICE);
+  s->h_ctl_init = (unsigned long long)n_slots;
+  HIP_TRY(hipMemcpyAsync(ctl + 2, &s->h_ctl_init, 8, hipMemcpyHostToDevice, stream), RT_EDEVICE);
 
   LogicArgs la{};
   Common c{};
@@ -850,7 +882,10 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.tiles_x = tiles_x;
   la.sub_x = tile_w / 8;
   la.n_pixels = n_pixels;
-  la.next_pixel = ctl + 1;
+  la.n_samples = n_samples;
+  la.n_units = n_units;
+  la.next_unit = (unsigned long long*)(ctl + 2);
+  la.samples = s->d_samples;
   la.out = d_out;
   la.n_slots = n_slots;
   la.state = s->d_state;
@@ -869,11 +904,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.qcount = ctl;
   ta.n_slots = n_slots;
   ta.stack_depth = s->desc.tree_depth + 2;
-  ta.counters = (unsigned long long*)(ctl + 4);
+  ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
   const size_t lds = (size_t)ta.stack_depth * kBlock * sizeof(int);
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, s->d_result);
+  hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result);
   HIP_TRY(hipGetLastError(), RT_EDEVICE);
 
   // ---- iterate logic -> trace until no slot issues a query
@@ -902,6 +937,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     ++iters;
     if (nq == 0) break;
   }
+  hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
+  HIP_TRY(hipGetLastError(), RT_EDEVICE);
   HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
   HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
   if (stats) {
