@@ -100,6 +100,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import ray_tracying_amd as rt
+    from ray_tracying_amd import tiles as tl
 
     dist = None
     if world > 1:
@@ -124,22 +125,22 @@ def main():
     W, H = scene.width, scene.height
     ds = rt.DeviceScene(scene, dev)
     T = args.tile
-    tiles_x, tiles_y = (W + T - 1) // T, (H + T - 1) // T
-    all_tiles = np.arange(tiles_x * tiles_y, dtype=np.int32)
-    mine = all_tiles[all_tiles % world == rank]
-    per_rank = (len(all_tiles) + world - 1) // world
-    out = torch.zeros(per_rank * T * T * 3, dtype=torch.float32, device=f"cuda:{dev}")
-    gather_list = [torch.empty_like(out) for _ in range(world)] if (dist and rank == 0) else None
+    tiles_x, tiles_y = tl.tile_grid(W, H, T)
+    n_tiles = tiles_x * tiles_y
+    mine = tl.assign_tiles(n_tiles, world, rank)
+    out = torch.zeros(tl.tiles_per_rank(n_tiles, world) * T * T * 3, dtype=torch.float32, device=f"cuda:{dev}")
+    gathered = None
     log(f"[rank {rank}] scene {W}x{H}, {scene.info.n_shapes} shapes, {scene.info.n_nodes} nodes, depth "
         f"{scene.info.tree_depth}, load+build {load_s:.1f} s; {len(mine)} tiles on cuda:{dev}")
 
     params = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=1, use_bvh=True, seed=args.seed)
 
     def step(seed):
+        nonlocal gathered
         params.seed = seed
         st = ds.render_tiles(mine, T, T, out.data_ptr(), params)
-        if dist:
-            dist.gather(out, gather_list, dst=0)
+        if dist:  # framebuffer gather to rank 0 over RCCL / xGMI
+            gathered = tl.gather_to_root(dist, out, rank, world)
         return st
 
     # ---- instrumented frame: algorithmic bytes per ray (same seed as the first timed step)
@@ -179,9 +180,9 @@ def main():
     rays_all, trace_ms_all, launches_all, alg_bytes_all = tot.tolist()
     elapsed = tmax.item()
 
-    if rank == 0 and dist:  # sanity: the gathered framebuffer covers every tile with finite values
-        packed = torch.stack(gather_list).cpu().numpy()
-        assert np.isfinite(packed).all()
+    if rank == 0 and dist:  # sanity: the gathered frame has every pixel, all finite
+        img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H)
+        assert np.isfinite(img).all()
 
     if rank != 0:
         if dist:

@@ -139,3 +139,38 @@ def cases() -> dict:
 def materialise(name: str, directory: str) -> tuple[str, dict]:
     builder, args = cases()[name]
     return write(copy.deepcopy(builder()), os.path.join(directory, name + ".json")), dict(args)
+
+
+def mirror_corridor(res=(40, 32)) -> dict:
+    """Two facing perfect mirrors + a glass cube (total internal reflection) and a glossy
+    sphere: drives the Trace recursion into MAX_RECURSION_DEPTH (raytracer.hpp:11)."""
+    mirror = {"diffuse_color": [0.9, 0.9, 0.9], "reflectivity": 0.95, "roughness": 0.0, "k_ambient": 0.05}
+    return {
+        "cameras": [{"location": [0.0, -1.0, 0.2], "gaze_vector": [0.35, 1.0, 0.05], "up_vector": [0, 0, 1],
+                     "focal_length": 30.0, "sensor_width": 36, "sensor_height": 24}],
+        "render": {"resolution_x": res[0], "resolution_y": res[1]},
+        "lights": [{"location": [0.0, 2.0, 1.5], "intensity": 300.0, "color": [1, 1, 1], "radius": 0.2}],
+        "rectangles": [
+            {"translation": [-1.0, 2.0, 0.0], "rotation": [0.0, 1.5707963, 0.0], "scale": [4.0, 8.0, 1.0], "material": mirror},
+            {"translation": [1.0, 2.0, 0.0], "rotation": [0.0, -1.5707963, 0.0], "scale": [4.0, 8.0, 1.0], "material": mirror},
+        ],
+        "cubes": [{"translation": [0.2, 3.0, 0.1], "rotation": [0.3, 0.5, 0.2], "scale": [0.5, 0.5, 0.5],
+                   "material": {"diffuse_color": [0.8, 0.9, 1.0], "transparency": 0.9, "refractive_index": 2.4,
+                                "reflectivity": 0.05}}],
+        "spheres": [{"location": [-0.3, 4.0, 0.3], "radius": 0.3,
+                     "material": {"reflectivity": 0.5, "roughness": 0.4}}],
+    }
+
+
+def tiny(n_prims=3, res=(21, 13)) -> dict:
+    """<= 4 primitives: the reference's BVH root is itself a leaf."""
+    s = soup(n_prims, seed=2, res=res)
+    s["spheres"] = [{"location": [0.0, 0.0, 0.0], "radius": 0.3}]
+    return s
+
+
+def empty(res=(16, 16)) -> dict:
+    return {"cameras": [{"location": [0, -4, 0], "gaze_vector": [0, 1, 0], "up_vector": [0, 0, 1],
+                         "focal_length": 35, "sensor_width": 36, "sensor_height": 36}],
+            "render": {"resolution_x": res[0], "resolution_y": res[1]},
+            "lights": [{"location": [0, 0, 3], "intensity": 100, "color": [1, 1, 1]}]}

@@ -1,0 +1,71 @@
+"""N>1 path on CPU: world_size-2 gloo run of the tile partition + gather + unpack used by
+bench.py (ray_tracying_amd/tiles.py).  Each rank renders ONLY its tiles (with the oracle as
+the per-tile renderer -- the GPU kernel is covered by test_gpu_parity); rank 0 gathers over
+torch.distributed and must reassemble a frame identical to the single-process render."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, scene_path, args, tile, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    from ray_tracying_amd import tiles as tl
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    W, H, _, _ = ob.scene_info(scene_path)
+    tx, ty = tl.tile_grid(W, H, tile)
+    n = tx * ty
+    mine = tl.assign_tiles(n, world, rank)
+    packed = np.zeros((tl.tiles_per_rank(n, world), tile, tile, 3), np.float32)
+    for k, tid in enumerate(mine):
+        x0, y0 = (tid % tx) * tile, (tid // tx) * tile
+        w, h = min(tile, W - x0), min(tile, H - y0)
+        rgb, _, _ = ob.render(scene_path, rng=ob.RNG_COUNTER, seed=5, region=(x0, y0, w, h), **args)
+        packed[k, :h, :w] = rgb
+    got = tl.gather_to_root(dist, torch.from_numpy(packed.reshape(-1)), rank, world)
+    if rank == 0:
+        q.put(tl.unpack([g.numpy() for g in got], world, n, tile, W, H))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tiles_gather_equals_single_render(world, tmp_path):
+    import multiprocessing as mp
+    import socket
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    import scenes
+    path, args = scenes.materialise("soup_s3", str(tmp_path))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, args, 8, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    img = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full, _, _ = ob.render(path, rng=ob.RNG_COUNTER, seed=5, **args)
+    assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
+
+
+def test_assign_tiles_is_a_partition():
+    from ray_tracying_amd import tiles as tl
+    for n in (1, 7, 256):
+        for world in (1, 2, 3, 8):
+            parts = [tl.assign_tiles(n, world, r) for r in range(world)]
+            allt = np.sort(np.concatenate(parts))
+            assert np.array_equal(allt, np.arange(n))
+            assert max(len(p) for p in parts) == tl.tiles_per_rank(n, world)

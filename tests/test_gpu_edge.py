@@ -1,0 +1,93 @@
+"""GPU edge cases against the oracle (counter RNG): recursion depth cap, TIR, degenerate BVHs,
+odd image sizes, spp edge values, linear mode, and tile-order independence."""
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import ray_tracying_amd as rt
+import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def check(path, tmp=None, seed=123, **args):
+    ref, _, ost = ob.render(path, rng=ob.RNG_COUNTER, seed=seed, texture_root=scenes.TEXTURES, **args)
+    sc = rt.Scene(path, texture_root=scenes.TEXTURES)
+    img, st = sc.render(rt.RenderParams(seed=seed, **args))
+    sc.close()
+    diff = int((img.view(np.uint32) != ref.view(np.uint32)).sum())
+    assert diff == 0, f"{diff} channels differ"
+    assert st.rays == ost["rays"]
+    return img, st
+
+
+@pytest.mark.parametrize("s", [1, 3])
+def test_mirror_corridor_depth_cap_and_tir(tmp_path, gpu, s):
+    p = scenes.write(scenes.mirror_corridor(), str(tmp_path / "m.json"))
+    check(p, use_bvh=True, spp_sqrt=s, light_samples=2)
+
+
+def test_root_is_leaf(tmp_path, gpu):
+    p = scenes.write(scenes.tiny(3), str(tmp_path / "t.json"))
+    check(p, use_bvh=True, spp_sqrt=2, light_samples=1)
+
+
+def test_empty_scene_is_background(tmp_path, gpu):
+    p = scenes.write(scenes.empty(), str(tmp_path / "e.json"))
+    img, st = check(p, use_bvh=True, spp_sqrt=1, light_samples=1)
+    assert np.all(img == np.float32(0.1))
+
+
+@pytest.mark.parametrize("res", [(37, 21), (1, 1), (65, 9)])
+def test_odd_resolutions(tmp_path, gpu, res):
+    p = scenes.write(scenes.features(res=res), str(tmp_path / "f.json"))
+    check(p, use_bvh=True, spp_sqrt=2, light_samples=1)
+
+
+@pytest.mark.parametrize("s", [0, -3, 1, 4])
+def test_spp_edge_values(tmp_path, gpu, s):
+    p = scenes.write(scenes.features(res=(24, 16)), str(tmp_path / "f.json"))
+    check(p, use_bvh=True, spp_sqrt=s, light_samples=1)
+
+
+def test_linear_mode_features(tmp_path, gpu):
+    p = scenes.write(scenes.features(res=(32, 24)), str(tmp_path / "f.json"))
+    check(p, use_bvh=False, spp_sqrt=2, light_samples=2)
+
+
+def test_larger_ascii_glossy(tmp_path, gpu):
+    p = scenes.write(scenes.ascii((128, 96)), str(tmp_path / "a.json"))
+    check(p, use_bvh=True, spp_sqrt=3, light_samples=1)
+
+
+def test_larger_soup(tmp_path, gpu):
+    p = scenes.write(scenes.soup(4000, seed=8, res=(96, 96)), str(tmp_path / "s.json"))
+    check(p, use_bvh=True, spp_sqrt=2, light_samples=1)
+
+
+def test_tile_order_and_subset_independence(tmp_path, gpu):
+    """Counter RNG: any tile list / order / device split renders bit-identical pixels."""
+    import torch
+    p = scenes.write(scenes.features(res=(64, 48)), str(tmp_path / "f.json"))
+    sc = rt.Scene(p, texture_root=scenes.TEXTURES)
+    full, _ = sc.render(rt.RenderParams(spp_sqrt=2, light_samples=2, seed=77))
+    ds = rt.DeviceScene(sc, 0)
+    T = 16
+    n = 4 * 3
+    order = np.array([7, 2, 11, 0, 5, 9, 1, 10, 3, 6, 8, 4], dtype=np.int32)
+    buf = torch.zeros(n * T * T * 3, dtype=torch.float32, device="cuda:0")
+    ds.render_tiles(order, T, T, buf.data_ptr(), rt.RenderParams(spp_sqrt=2, light_samples=2, seed=77))
+    img = rt.unpack_tiles(buf.cpu().numpy(), order, T, T, 64, 48)
+    assert np.array_equal(img.view(np.uint32), full.view(np.uint32))
+    # two "ranks" worth of tiles rendered separately
+    from ray_tracying_amd import tiles as tl
+    parts = []
+    for r in range(2):
+        mine = tl.assign_tiles(n, 2, r)
+        b = torch.zeros(tl.tiles_per_rank(n, 2) * T * T * 3, dtype=torch.float32, device="cuda:0")
+        ds.render_tiles(mine, T, T, b.data_ptr(), rt.RenderParams(spp_sqrt=2, light_samples=2, seed=77))
+        parts.append(b.cpu().numpy())
+    img2 = tl.unpack(parts, 2, n, T, 64, 48)
+    assert np.array_equal(img2.view(np.uint32), full.view(np.uint32))
+    ds.close()
+    sc.close()
