@@ -22,7 +22,7 @@ $(LIB)/librt_hip.so: $(SRC)/hip/rt_hip.hip $(SRC)/hip/rt_device.h $(COMMON_H)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared $(SRC)/hip/rt_hip.hip -o $@
 
-HOST_SRC := $(SRC)/host/json_dom.cpp $(SRC)/host/scene.cpp $(SRC)/host/rt_host_api.cpp
+HOST_SRC := $(SRC)/host/json_dom.cpp $(SRC)/host/scene.cpp $(SRC)/host/bvh_wide.cpp $(SRC)/host/rt_host_api.cpp
 $(LIB)/librt_host.so: $(HOST_SRC) $(SRC)/host/json_dom.hpp $(SRC)/host/scene.hpp include/rt_host.h $(COMMON_H) $(LIB)/librt_hip.so
 	$(CXX) $(CXXFLAGS) -shared $(HOST_SRC) -o $@ -L$(LIB) -lrt_hip -Wl,-rpath,'$$ORIGIN'
 

@@ -55,24 +55,33 @@ extern "C" {
  * Plane (shapes.cpp:444-494; a triangle is a Plane with c3 == c0):
  *   a[0..2]=c0 a[3]=n.x  a[4..6]=c1 a[7]=n.y  a[8..10]=c2 a[11]=n.z  a[12..14]=c3 a[15]=tag
  *   n = normalize(cross(c1-c0, c2-c0)), computed on the host with the reference's ops.
- * Records are stored in the reference's BVH-sorted order (acceleration.cpp:46-55): the
- * record index is the tie-break order for equal hit distances. */
+ * Records are stored in traversal order; rt_prim_ref gives each one's reference order. */
 typedef struct rt_prim {
   float a[16];
   float b[16];
 } rt_prim;
 
-/* BVH2 node, 64 bytes: the boxes of both children plus their references.
- *   box[0..5]  = left  child lo.xyz, hi.xyz;  box[6..11] = right child lo.xyz, hi.xyz
- *   ref > = 0 : internal child node index (its box is padded, tested conservatively)
- *   cnt > 0   : leaf child; ref = first primitive, cnt = 1..4 primitives; its box is the
- *               reference's exact leaf AABB and is tested with AABB::intersect semantics
- *               (shapes.cpp:55-72) so the set of candidate primitives is the reference's.
- *   ref == -1 && cnt == 0 : no child. */
-typedef struct rt_node {
-  float box[12];
-  int32_t ref_l, ref_r, cnt_l, cnt_r;
-} rt_node;
+/* Traversal node: 4-wide, 128 bytes (one cache line), children's boxes in SoA order.
+ * Built on the host with binned SAH over conservative per-primitive hit boxes
+ * (bvh_wide.cpp); the reference's own median-split tree (acceleration.cpp:20-64) is NOT used
+ * for traversal -- its leaves survive as rt_prim_ref.ref_leaf / ref_leaf_boxes, the exact
+ * filter every candidate hit must pass (AABB::intersect, shapes.cpp:55-72).
+ *   meta byte k: 0 = no child; 0x01 = internal child (child[k] = node index);
+ *                0x80 | n = leaf child with n primitives starting at child[k]. */
+typedef struct rt_node4 {
+  float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
+  int32_t child[4];
+  uint32_t meta;
+  uint32_t pad[3];
+} rt_node4;
+
+/* Per primitive (in traversal order): its position in the reference's BVH-sorted list
+ * (the tie-break order for equal t, acceleration.cpp:112/133) and the reference leaf that
+ * holds it (index into ref_leaf_boxes). */
+typedef struct rt_prim_ref {
+  int32_t ref_index;
+  int32_t ref_leaf;
+} rt_prim_ref;
 
 /* Material (material.hpp:47-93 after json_loader.cpp:30-97), 64 bytes. */
 typedef struct rt_material {
@@ -98,11 +107,16 @@ typedef struct rt_texture {
 
 typedef struct rt_scene_desc {
   int32_t n_prims;
-  int32_t prim_stride; /* 64 (all planes) or 128 bytes */
-  const rt_prim* prims; /* n_prims records at prim_stride */
-  int32_t n_nodes;      /* 0 when n_prims == 0 */
-  int32_t tree_depth;   /* max root->leaf node count, sizes the LDS traversal stack */
-  const rt_node* nodes;
+  int32_t prim_stride;          /* 64 (all planes) or 128 bytes */
+  const rt_prim* prims;         /* n_prims records at prim_stride, traversal order */
+  const rt_prim_ref* prim_refs; /* n_prims */
+  int32_t n_unbounded;          /* the last n_unbounded prims are tested by every ray */
+  int32_t n_nodes;              /* 0 when no bounded primitive */
+  int32_t tree_depth;           /* node levels of the 4-wide tree */
+  int32_t stack_bound;          /* max traversal stack entries (3 per level + 2) */
+  const rt_node4* nodes;
+  int32_t n_ref_leaves;
+  const float* ref_leaf_boxes;  /* n_ref_leaves x {lo.x, lo.y, lo.z, 0, hi.x, hi.y, hi.z, 0} */
   int32_t n_materials;
   const rt_material* materials;
   int32_t n_lights;
@@ -112,7 +126,7 @@ typedef struct rt_scene_desc {
   int64_t n_texel_bytes;
   const uint8_t* texels;
   float scene_scale; /* max |coordinate| of scene bounds and camera, for pruning margins */
-  int32_t flags;     /* RT_SCENE_* feature bits (select kernel variants) */
+  int32_t flags;     /* RT_SCENE_* feature bits */
 } rt_scene_desc;
 
 #define RT_SCENE_HAS_REFLECTION 1

@@ -39,7 +39,10 @@ class NativeError(RuntimeError):
 class rt_scene_desc(ctypes.Structure):
     _fields_ = [
         ("n_prims", ctypes.c_int32), ("prim_stride", ctypes.c_int32), ("prims", ctypes.c_void_p),
-        ("n_nodes", ctypes.c_int32), ("tree_depth", ctypes.c_int32), ("nodes", ctypes.c_void_p),
+        ("prim_refs", ctypes.c_void_p), ("n_unbounded", ctypes.c_int32),
+        ("n_nodes", ctypes.c_int32), ("tree_depth", ctypes.c_int32), ("stack_bound", ctypes.c_int32),
+        ("nodes", ctypes.c_void_p),
+        ("n_ref_leaves", ctypes.c_int32), ("ref_leaf_boxes", ctypes.c_void_p),
         ("n_materials", ctypes.c_int32), ("materials", ctypes.c_void_p),
         ("n_lights", ctypes.c_int32), ("lights", ctypes.c_void_p),
         ("n_textures", ctypes.c_int32), ("textures", ctypes.c_void_p),

@@ -40,6 +40,7 @@ namespace {
 
 constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
 constexpr int kBlock = 256;
+constexpr int kLdsStack = 16;  // traversal stack entries per lane held in LDS (rest spill to HBM)
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
@@ -107,48 +108,93 @@ struct LogicArgs {
 
 struct TraceArgs {
   Common c;
+  const int2* prim_refs;      // (reference index, reference leaf) per primitive
+  const float4* ref_boxes;    // 2 float4 per reference leaf: lo, hi
+  int n_unbounded;
+  int n_nodes;
   const float* query;
   int* result;
   const int* qlist;
   const unsigned int* qcount;
+  unsigned int* fetch;        // persistent work counter (zeroed per launch)
   int n_slots;
-  int stack_depth;
+  int lds_entries;            // traversal stack entries kept in LDS per lane
+  int* spill;                 // deeper entries: [entry - lds_entries][n_threads]
+  int n_threads;              // threads of the persistent grid
   unsigned long long* counters;  // box tests, prim tests (count_work)
 };
 
 // ---------------------------------------------------------------- traversal
+// The closest-hit / any-hit state of one query.
+struct HitState {
+  float best_t;
+  int best_ref;   // reference index of the best hit (tie-break, acceleration.cpp:112)
+  int best_idx;   // primitive index (traversal order) of the best hit, -1 = miss
+  bool done;      // any-hit: occluded
+};
+
+// The reference accepts a primitive's hit only if its reference leaf box passes the exact
+// AABB::intersect (acceleration.cpp:71-75); checked lazily, for candidate hits only.
+__device__ __forceinline__ bool ref_leaf_ok(const TraceArgs& a, int leaf, const Ray& r, uint32_t par) {
+  const float4 lo = a.ref_boxes[2 * leaf], hi = a.ref_boxes[2 * leaf + 1];
+  const float blo[3] = {lo.x, lo.y, lo.z}, bhi[3] = {hi.x, hi.y, hi.z};
+  float tn;
+  return aabb_exact(blo, bhi, r, par, tn);
+}
+
 template <bool kCount>
-__device__ __forceinline__ void test_prims(const Common& a, int first, int cnt, const Ray& r, bool any,
-                                           float tmax, int& best_idx, float& best_t, bool& done,
-                                           unsigned int& nprim) {
+__device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cnt, const Ray& r, bool any, float tmax,
+                                           uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
   for (int k = 0; k < cnt; ++k) {
-    int pi = first + k;
-    const float4* rec = a.prims + (size_t)pi * a.prim_stride4;
+    const int pi = first + k;
+    const float4* rec = a.c.prims + (size_t)pi * a.c.prim_stride4;
     PrimA P;
     load_prim_a(rec, P);
     float t;
     if (kCount) ++nprim;
-    if (prim_hit<false>(P, rec, r, t, nullptr)) {
-      if (any) {
-        if (!(t > tmax)) { done = true; return; }  // occludes: t <= light_dist
-      } else if (t < best_t || (t == best_t && pi < best_idx)) {
-        best_t = t;
-        best_idx = pi;
+    if (!prim_hit<false>(P, rec, r, t, nullptr)) continue;
+    const int2 ref = a.prim_refs[pi];
+    if (any) {  // occluder iff t <= light_dist (raytracer.cpp:233)
+      if (!(t > tmax) && (!check_leaf || ref_leaf_ok(a, ref.y, r, par))) {
+        h.done = true;
+        return;
       }
+    } else if ((t < h.best_t || (t == h.best_t && ref.x < h.best_ref)) &&
+               (!check_leaf || ref_leaf_ok(a, ref.y, r, par))) {
+      h.best_t = t;
+      h.best_ref = ref.x;
+      h.best_idx = pi;
     }
   }
+}
+
+__device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
+  const bool sw = tb < ta;
+  const float t = sw ? tb : ta;
+  const int c = sw ? cb : ca;
+  tb = sw ? ta : tb;
+  cb = sw ? ca : cb;
+  ta = t;
+  ca = c;
 }
 
 template <bool kCount>
 __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
-  const int i = blockIdx.x * kBlock + threadIdx.x;
   const unsigned int nq = *ta.qcount;
+  const int lane = threadIdx.x & 63;
+  const int gtid = blockIdx.x * kBlock + threadIdx.x;
   unsigned int nbox = 0, nprim = 0;
-  if ((unsigned)i < nq) {
-    const Common& a = ta.c;
-    const int slot = ta.qlist[i];
-    const int N = ta.n_slots;
+  const TraceArgs& a = ta;
+  const int N = ta.n_slots;
+  for (;;) {  // persistent: each wave pulls 64 queries at a time
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(ta.fetch, 64u);
+    base = __shfl(base, 0);
+    if (base >= nq) break;
+    const unsigned int qi = base + lane;
+    if (qi >= nq) continue;
+    const int slot = ta.qlist[qi];
     Ray r;
     r.o = V3{ta.query[(Q_O + 0) * N + slot], ta.query[(Q_O + 1) * N + slot], ta.query[(Q_O + 2) * N + slot]};
     r.d = V3{ta.query[(Q_D + 0) * N + slot], ta.query[(Q_D + 1) * N + slot], ta.query[(Q_D + 2) * N + slot]};
@@ -157,69 +203,93 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
     const bool any = (kind & 1) != 0;
     const float tmax = any ? tq : 0.0f;
     r.time = any ? 0.0f : tq;  // shadow rays have time 0 (raytracer.cpp:225, shapes.hpp:28)
-    int best_idx = -1;
-    float best_t = __builtin_inff();
-    bool done = false;
-    if (a.n_prims > 0) {
-      if (!a.use_bvh) {  // BVH::intersect_linear (acceleration.cpp:124-139)
-        test_prims<kCount>(a, 0, a.n_prims, r, any, tmax, best_idx, best_t, done, nprim);
-      } else {
-        uint32_t par = 0;
-        par |= ((double)fabsf(r.d.x) < 1e-6) ? 1u : 0u;
-        par |= ((double)fabsf(r.d.y) < 1e-6) ? 2u : 0u;
-        par |= ((double)fabsf(r.d.z) < 1e-6) ? 4u : 0u;
-        auto safe_inv = [](float d) {
-          float dd = fabsf(d) < 1e-12f ? copysignf(1e-12f, d) : d;
-          return 1.0f / dd;
-        };
-        const V3 inv{safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z)};
-        int* stack = lds_stack + threadIdx.x;
-        int sp = 0, node = 0;
-        while (true) {
-          const float4* nd = a.nodes + (size_t)node * 4;
-          const float4 n0 = nd[0], n1 = nd[1], n2 = nd[2];
-          const int4 nr = *reinterpret_cast<const int4*>(nd + 3);
-          const float bl_lo[3] = {n0.x, n0.y, n0.z}, bl_hi[3] = {n0.w, n1.x, n1.y};
-          const float br_lo[3] = {n1.z, n1.w, n2.x}, br_hi[3] = {n2.y, n2.z, n2.w};
-          float lim = any ? tmax : best_t;
-          lim = lim + (lim * 1e-5f + a.eps_abs);
-          bool hl = false, hr = false;
-          float tl = 0.f, tr = 0.f;
-          if (nr.z > 0) hl = aabb_exact(bl_lo, bl_hi, r, par, tl);
-          else if (nr.x >= 0) hl = aabb_fast(bl_lo, bl_hi, r.o, inv, tl);
-          if (nr.w > 0) hr = aabb_exact(br_lo, br_hi, r, par, tr);
-          else if (nr.y >= 0) hr = aabb_fast(br_lo, br_hi, r.o, inv, tr);
-          if (kCount) nbox += (nr.z > 0 || nr.x >= 0) + (nr.w > 0 || nr.y >= 0);
-          hl = hl && !(tl > lim);
-          hr = hr && !(tr > lim);
-          if (hl && nr.z > 0) {
-            test_prims<kCount>(a, nr.x, nr.z, r, any, tmax, best_idx, best_t, done, nprim);
-            hl = false;
-            if (done) break;
-          }
-          if (hr && nr.w > 0) {
-            test_prims<kCount>(a, nr.y, nr.w, r, any, tmax, best_idx, best_t, done, nprim);
-            hr = false;
-            if (done) break;
-          }
-          if (hl && hr) {
-            const bool lf = tl <= tr;
-            stack[sp * kBlock] = lf ? nr.y : nr.x;
-            ++sp;
-            node = lf ? nr.x : nr.y;
-          } else if (hl) {
-            node = nr.x;
-          } else if (hr) {
-            node = nr.y;
-          } else {
-            if (sp == 0) break;
-            --sp;
-            node = stack[sp * kBlock];
+    HitState h{__builtin_inff(), 0x7fffffff, -1, false};
+    uint32_t par = 0;
+    par |= ((double)fabsf(r.d.x) < 1e-6) ? 1u : 0u;
+    par |= ((double)fabsf(r.d.y) < 1e-6) ? 2u : 0u;
+    par |= ((double)fabsf(r.d.z) < 1e-6) ? 4u : 0u;
+    if (a.c.n_prims > 0 && !a.c.use_bvh) {  // BVH::intersect_linear (acceleration.cpp:124-139)
+      test_prims<kCount>(a, 0, a.c.n_prims, r, any, tmax, par, false, h, nprim);
+    } else if (a.c.n_prims > 0) {
+      auto safe_inv = [](float d) {
+        float dd = fabsf(d) < 1e-12f ? copysignf(1e-12f, d) : d;
+        return 1.0f / dd;
+      };
+      const V3 inv{safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z)};
+      int* lstack = lds_stack + threadIdx.x;
+      int sp = 0;
+      int node = a.n_nodes > 0 ? 0 : -1;
+      while (node >= 0) {
+        const float4* nd = a.c.nodes + (size_t)node * 8;
+        const float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5];
+        const int4 ch = *reinterpret_cast<const int4*>(nd + 6);
+        const uint32_t meta = *reinterpret_cast<const uint32_t*>(nd + 7);
+        const float clx[4] = {lx.x, lx.y, lx.z, lx.w}, chx[4] = {hx.x, hx.y, hx.z, hx.w};
+        const float cly[4] = {ly.x, ly.y, ly.z, ly.w}, chy[4] = {hy.x, hy.y, hy.z, hy.w};
+        const float clz[4] = {lz.x, lz.y, lz.z, lz.w}, chz[4] = {hz.x, hz.y, hz.z, hz.w};
+        const int cc[4] = {ch.x, ch.y, ch.z, ch.w};
+        float tn[4];
+        bool hit[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float tx1 = (clx[k] - r.o.x) * inv.x, tx2 = (chx[k] - r.o.x) * inv.x;
+          const float ty1 = (cly[k] - r.o.y) * inv.y, ty2 = (chy[k] - r.o.y) * inv.y;
+          const float tz1 = (clz[k] - r.o.z) * inv.z, tz2 = (chz[k] - r.o.z) * inv.z;
+          const float n0 = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+          const float f0 = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+          tn[k] = n0;
+          hit[k] = ((meta >> (8 * k)) & 0xffu) != 0 && n0 <= f0 && f0 >= 0.0f;
+        }
+        if (kCount) nbox += __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
+                                                (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
+        // leaves first (their hits tighten the bound before internal children are ordered)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t m = (meta >> (8 * k)) & 0xffu;
+          if (hit[k] && (m & 0x80u)) {
+            float lim = any ? tmax : h.best_t;
+            lim = lim + (lim * 1e-5f + a.c.eps_abs);
+            if (!(tn[k] > lim)) test_prims<kCount>(a, cc[k], (int)(m & 0x7fu), r, any, tmax, par, true, h, nprim);
+            hit[k] = false;
           }
         }
+        if (h.done) break;
+        float lim = any ? tmax : h.best_t;
+        lim = lim + (lim * 1e-5f + a.c.eps_abs);
+        float t0 = __builtin_inff(), t1 = __builtin_inff(), t2 = __builtin_inff(), t3 = __builtin_inff();
+        int c0 = -1, c1 = -1, c2 = -1, c3 = -1;
+        if (hit[0] && !(tn[0] > lim)) { t0 = tn[0]; c0 = cc[0]; }
+        if (hit[1] && !(tn[1] > lim)) { t1 = tn[1]; c1 = cc[1]; }
+        if (hit[2] && !(tn[2] > lim)) { t2 = tn[2]; c2 = cc[2]; }
+        if (hit[3] && !(tn[3] > lim)) { t3 = tn[3]; c3 = cc[3]; }
+        // sort 4 (t, child) ascending; misses (-1, inf) sink to the end
+        cswap(t0, c0, t1, c1);
+        cswap(t2, c2, t3, c3);
+        cswap(t0, c0, t2, c2);
+        cswap(t1, c1, t3, c3);
+        cswap(t1, c1, t2, c2);
+        auto push = [&](int v) {
+          if (sp < a.lds_entries) lstack[sp * kBlock] = v;
+          else a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = v;
+          ++sp;
+        };
+        if (c3 >= 0) push(c3);
+        if (c2 >= 0) push(c2);
+        if (c1 >= 0) push(c1);
+        if (c0 >= 0) {
+          node = c0;
+        } else if (sp > 0) {
+          --sp;
+          node = sp < a.lds_entries ? lstack[sp * kBlock] : a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid];
+        } else {
+          node = -1;
+        }
       }
+      // primitives whose accepted region is not boxable: tested by every ray
+      if (!h.done && a.n_unbounded > 0)
+        test_prims<kCount>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, any, tmax, par, true, h, nprim);
     }
-    ta.result[slot] = any ? (done ? 1 : 0) : best_idx;
+    ta.result[slot] = any ? (h.done ? 1 : 0) : h.best_idx;
   }
   if (kCount) {
     unsigned long long b = nbox, p = nprim;
@@ -227,7 +297,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
       b += __shfl_xor(b, off);
       p += __shfl_xor(p, off);
     }
-    if ((threadIdx.x & 63) == 0 && (b | p)) {
+    if (lane == 0 && (b | p)) {
       atomicAdd(ta.counters + 0, b);
       atomicAdd(ta.counters + 1, p);
     }
@@ -691,8 +761,13 @@ struct rt_scene_s {
   void* d_lights = nullptr;
   void* d_tex = nullptr;
   void* d_texels = nullptr;
+  void* d_prim_refs = nullptr;
+  void* d_ref_boxes = nullptr;
+  int n_cu = 0, trace_blocks_per_cu = 0;
+  int* d_spill = nullptr;
+  size_t spill_cap = 0;
   // per-render workspace (grown on demand)
-  void* d_ctl = nullptr;  // bytes 0: qcount (u32), 8: next_unit (u64), 16/24: box/prim tests (u64)
+  void* d_ctl = nullptr;  // bytes 0: qcount (u32), 4: trace fetch (u32), 8: next_unit (u64), 16/24: box/prim (u64)
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
   uint32_t* d_state = nullptr;
@@ -753,7 +828,8 @@ int rt_scene_destroy(rt_scene_t s) {
   (void)hipSetDevice(s->device);
   (void)hipDeviceSynchronize();
   free_workspace(s);
-  void* ptrs[] = {s->d_prims, s->d_nodes, s->d_mats, s->d_lights, s->d_tex, s->d_texels, s->d_ctl, s->d_tiles};
+  void* ptrs[] = {s->d_prims, s->d_nodes, s->d_mats, s->d_lights, s->d_tex, s->d_texels, s->d_ctl, s->d_tiles,
+                  s->d_prim_refs, s->d_ref_boxes, s->d_spill};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_qcount) (void)hipHostFree(s->h_qcount);
@@ -766,13 +842,15 @@ int rt_scene_destroy(rt_scene_t s) {
 
 int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   if (!d || !out) return fail(RT_EINVAL, "rt_scene_create: null argument");
-  if (d->n_prims < 0 || (d->n_prims > 0 && (!d->prims || d->n_nodes <= 0 || !d->nodes)))
+  if (d->n_prims < 0 || (d->n_prims > 0 && (!d->prims || !d->prim_refs)) ||
+      (d->n_prims > d->n_unbounded && (d->n_nodes <= 0 || !d->nodes)) || d->n_unbounded < 0 ||
+      d->n_unbounded > d->n_prims || (d->n_prims > 0 && (d->n_ref_leaves <= 0 || !d->ref_leaf_boxes)))
     return fail(RT_EINVAL, "rt_scene_create: inconsistent primitive/node arrays");
+  if (d->stack_bound < 1 || d->stack_bound > 4096) return fail(RT_EINVAL, "rt_scene_create: stack_bound out of range");
   if (d->prim_stride != 64 && d->prim_stride != 128)
     return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
   if (d->n_materials <= 0 || !d->materials) return fail(RT_EINVAL, "rt_scene_create: need >= 1 material");
   if (d->n_lights < 0 || (d->n_lights > 0 && !d->lights)) return fail(RT_EINVAL, "rt_scene_create: bad lights");
-  if (d->tree_depth < 0 || d->tree_depth > 64) return fail(RT_EINVAL, "rt_scene_create: tree_depth out of range");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
     return fail(RT_ENODEV, "rt_scene_create: no such HIP device");
@@ -782,7 +860,9 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   s->desc = *d;
   int rc = RT_OK;
   if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
-      (rc = upload(&s->d_nodes, d->nodes, (size_t)d->n_nodes * sizeof(rt_node))) ||
+      (rc = upload(&s->d_nodes, d->nodes, (size_t)d->n_nodes * sizeof(rt_node4))) ||
+      (rc = upload(&s->d_prim_refs, d->prim_refs, (size_t)d->n_prims * sizeof(rt_prim_ref))) ||
+      (rc = upload(&s->d_ref_boxes, d->ref_leaf_boxes, (size_t)d->n_ref_leaves * 8 * sizeof(float))) ||
       (rc = upload(&s->d_mats, d->materials, (size_t)d->n_materials * sizeof(rt_material))) ||
       (rc = upload(&s->d_lights, d->lights, (size_t)d->n_lights * sizeof(rt_light))) ||
       (rc = upload(&s->d_tex, d->textures, (size_t)d->n_textures * sizeof(rt_texture))) ||
@@ -796,7 +876,18 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     rt_scene_destroy(s);
     return fail(RT_ENOMEM, "rt_scene_create: control block / events");
   }
-  s->desc.prims = nullptr; s->desc.nodes = nullptr; s->desc.materials = nullptr;
+  {  // persistent trace grid: blocks resident per CU x CUs
+    int ncu = 0, bpc = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
+    const int lds_entries = std::min(d->stack_bound, kLdsStack);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<false>, kBlock,
+                                                     (size_t)lds_entries * kBlock * sizeof(int)) != hipSuccess || bpc < 1)
+      bpc = 2;
+    s->n_cu = ncu;
+    s->trace_blocks_per_cu = bpc;
+  }
+  s->desc.prims = nullptr; s->desc.nodes = nullptr; s->desc.materials = nullptr; s->desc.prim_refs = nullptr;
+  s->desc.ref_leaf_boxes = nullptr;
   s->desc.lights = nullptr; s->desc.textures = nullptr; s->desc.texels = nullptr;
   *out = s;
   return RT_OK;
@@ -898,14 +989,31 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
 
   TraceArgs ta{};
   ta.c = c;
+  ta.prim_refs = (const int2*)s->d_prim_refs;
+  ta.ref_boxes = (const float4*)s->d_ref_boxes;
+  ta.n_unbounded = s->desc.n_unbounded;
+  ta.n_nodes = s->desc.n_nodes;
   ta.query = s->d_query;
   ta.result = s->d_result;
   ta.qlist = s->d_qlist;
   ta.qcount = ctl;
+  ta.fetch = ctl + 1;
   ta.n_slots = n_slots;
-  ta.stack_depth = s->desc.tree_depth + 2;
+  ta.lds_entries = std::min(s->desc.stack_bound, kLdsStack);
+  const unsigned trace_blocks = (unsigned)std::max(1, std::min(s->n_cu * s->trace_blocks_per_cu,
+                                                               (n_slots + kBlock - 1) / kBlock));
+  ta.n_threads = (int)trace_blocks * kBlock;
+  const int spill_entries = std::max(0, s->desc.stack_bound - ta.lds_entries);
+  if ((size_t)spill_entries * ta.n_threads > s->spill_cap) {
+    if (s->d_spill) (void)hipFree(s->d_spill);
+    s->d_spill = nullptr;
+    s->spill_cap = 0;
+    HIP_TRY(hipMalloc(&s->d_spill, (size_t)spill_entries * ta.n_threads * sizeof(int)), RT_ENOMEM);
+    s->spill_cap = (size_t)spill_entries * ta.n_threads;
+  }
+  ta.spill = s->d_spill;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
-  const size_t lds = (size_t)ta.stack_depth * kBlock * sizeof(int);
+  const size_t lds = (size_t)ta.lds_entries * kBlock * sizeof(int);
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result);
@@ -917,15 +1025,15 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   int iters = 0;
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
   for (;;) {
-    HIP_TRY(hipMemsetAsync(ctl, 0, 4, stream), RT_EDEVICE);
+    HIP_TRY(hipMemsetAsync(ctl, 0, 8, stream), RT_EDEVICE);  // qcount + trace fetch counter
     hipLaunchKernelGGL(logic_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipMemcpyAsync(s->h_qcount, ctl, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
     if (p->count_work)
-      hipLaunchKernelGGL(trace_kernel<true>, dim3(slot_blocks), dim3(kBlock), lds, stream, ta);
+      hipLaunchKernelGGL(trace_kernel<true>, dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
     else
-      hipLaunchKernelGGL(trace_kernel<false>, dim3(slot_blocks), dim3(kBlock), lds, stream, ta);
+      hipLaunchKernelGGL(trace_kernel<false>, dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
     HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);

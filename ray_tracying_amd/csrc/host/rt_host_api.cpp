@@ -82,7 +82,7 @@ int rth_scene_get_info(rth_scene_t h, rth_scene_info* info) {
   info->height = s.camera.res_y;
   info->n_shapes = (int32_t)s.shapes.size();
   info->n_lights = (int32_t)s.lights.size();
-  info->n_nodes = (int32_t)s.nodes.size();
+  info->n_nodes = (int32_t)s.node4.size();
   info->tree_depth = s.tree_depth;
   info->n_materials = (int32_t)s.materials.size();
   info->n_textures = (int32_t)s.textures.size();

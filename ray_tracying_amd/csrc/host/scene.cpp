@@ -553,73 +553,29 @@ void build_bvh(Scene& sc) {
   }
   if (sc.materials.empty()) sc.materials.push_back(rt_material{});  // placeholder for empty scenes
   sc.prim_stride = (n > 0 && all_planes) ? 64 : 128;
-  {
-    const size_t fl = (size_t)sc.prim_stride / 4;
-    sc.prim_blob.assign((size_t)n * fl, 0.0f);
-    for (int k = 0; k < n; ++k) std::memcpy(&sc.prim_blob[(size_t)k * fl], &sc.prims[k], (size_t)sc.prim_stride);
-  }
 
   // scale for pruning / padding margins: scene boxes and the camera
   for (const BNode& nd : B.nodes)
     for (int i = 0; i < 3; ++i) scale = finite_abs_max(finite_abs_max(scale, nd.box.lo[i]), nd.box.hi[i]);
   for (int i = 0; i < 3; ++i) scale = finite_abs_max(scale, sc.camera.location[i]);
   sc.scene_scale = scale;
-  const float pad = 1e-5f * scale;
 
-  // flatten: one rt_node per internal reference node (DFS order, left subtree first)
-  sc.nodes.clear();
+  // the reference's leaves: exact boxes + which leaf holds each sorted position
+  std::vector<int> ref_leaf_of(n, 0);
+  sc.ref_leaf_boxes.clear();
+  for (const BNode& nd : B.nodes) {
+    if (!nd.leaf()) continue;
+    int id = (int)(sc.ref_leaf_boxes.size() / 8);
+    for (int i = nd.start; i < nd.end; ++i) ref_leaf_of[i] = id;
+    const float v[8] = {nd.box.lo[0], nd.box.lo[1], nd.box.lo[2], 0.0f, nd.box.hi[0], nd.box.hi[1], nd.box.hi[2], 0.0f};
+    sc.ref_leaf_boxes.insert(sc.ref_leaf_boxes.end(), v, v + 8);
+  }
   sc.tree_depth = 0;
-  if (n > 0) {
-    auto child = [&](int c, float* box, int32_t& ref, int32_t& cnt, std::vector<std::pair<int, int>>& todo, int depth) {
-      const BNode& b = B.nodes[c];
-      if (b.leaf()) {
-        for (int i = 0; i < 3; ++i) { box[i] = b.box.lo[i]; box[3 + i] = b.box.hi[i]; }
-        ref = b.start;
-        cnt = b.end - b.start;
-      } else {
-        for (int i = 0; i < 3; ++i) { box[i] = b.box.lo[i] - pad; box[3 + i] = b.box.hi[i] + pad; }
-        ref = -2;  // patched when the child gets its index
-        cnt = 0;
-        todo.push_back({c, depth});
-      }
-    };
-    // iterative DFS; each entry: (reference node id, depth), with the parent slot to patch
-    struct Item { int bnode; int depth; int parent; int side; };
-    std::vector<Item> stack;
-    stack.push_back({0, 1, -1, 0});
-    while (!stack.empty()) {
-      Item it = stack.back();
-      stack.pop_back();
-      int id = (int)sc.nodes.size();
-      sc.nodes.emplace_back();
-      if (it.parent >= 0) {
-        if (it.side == 0) sc.nodes[it.parent].ref_l = id;
-        else sc.nodes[it.parent].ref_r = id;
-      }
-      sc.tree_depth = std::max(sc.tree_depth, it.depth);
-      const BNode& b = B.nodes[it.bnode];
-      rt_node& out = sc.nodes[id];
-      std::vector<std::pair<int, int>> todo;
-      if (b.leaf()) {  // whole scene is one leaf: left = that leaf, right = none
-        child(it.bnode, out.box, out.ref_l, out.cnt_l, todo, it.depth + 1);
-        for (int i = 0; i < 6; ++i) out.box[6 + i] = 0.0f;
-        out.ref_r = -1;
-        out.cnt_r = 0;
-        continue;
-      }
-      int32_t rl, cl, rr, cr;
-      float bl[6], br[6];
-      std::vector<std::pair<int, int>> tl, tr;
-      child(b.left, bl, rl, cl, tl, it.depth + 1);
-      child(b.right, br, rr, cr, tr, it.depth + 1);
-      rt_node& o2 = sc.nodes[id];
-      std::copy(bl, bl + 6, o2.box);
-      std::copy(br, br + 6, o2.box + 6);
-      o2.ref_l = rl; o2.cnt_l = cl; o2.ref_r = rr; o2.cnt_r = cr;
-      // push right first so the left subtree is laid out right after its parent
-      if (!tr.empty()) stack.push_back({b.right, it.depth + 1, id, 1});
-      if (!tl.empty()) stack.push_back({b.left, it.depth + 1, id, 0});
-    }
+  build_wide(sc, boxes, ref_leaf_of);
+  {
+    const size_t fl = (size_t)sc.prim_stride / 4;
+    sc.prim_blob.assign((size_t)n * fl, 0.0f);
+    for (int k = 0; k < n; ++k) std::memcpy(&sc.prim_blob[(size_t)k * fl], &sc.prims[k], (size_t)sc.prim_stride);
   }
   sc.flags = flags;
 
@@ -671,9 +627,14 @@ rt_scene_desc scene_desc(const Scene& sc) {
   d.n_prims = (int32_t)sc.prims.size();
   d.prim_stride = sc.prim_stride;
   d.prims = reinterpret_cast<const rt_prim*>(sc.prim_blob.data());
-  d.n_nodes = (int32_t)sc.nodes.size();
+  d.prim_refs = sc.prim_refs.data();
+  d.n_unbounded = sc.n_unbounded;
+  d.n_nodes = (int32_t)sc.node4.size();
   d.tree_depth = sc.tree_depth;
-  d.nodes = sc.nodes.data();
+  d.stack_bound = sc.stack_bound;
+  d.nodes = sc.node4.data();
+  d.n_ref_leaves = (int32_t)(sc.ref_leaf_boxes.size() / 8);
+  d.ref_leaf_boxes = sc.ref_leaf_boxes.data();
   d.n_materials = (int32_t)sc.materials.size();
   d.materials = sc.materials.data();
   d.n_lights = (int32_t)sc.lights.size();

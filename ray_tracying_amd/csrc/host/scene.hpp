@@ -59,9 +59,13 @@ struct Scene {
   std::vector<Texture> textures;
   // flattened
   std::vector<int> order;          // BVH-sorted shape indices (acceleration.cpp:46-55)
-  std::vector<rt_prim> prims;      // in sorted order
+  std::vector<rt_prim> prims;      // traversal order (after build_wide)
   std::vector<float> prim_blob;    // prims packed at prim_stride bytes (what the device reads)
-  std::vector<rt_node> nodes;
+  std::vector<rt_node4> node4;        // traversal tree (bvh_wide.cpp)
+  std::vector<rt_prim_ref> prim_refs;  // per prim (traversal order)
+  std::vector<float> ref_leaf_boxes;   // 8 floats per reference leaf
+  int n_unbounded = 0;
+  int stack_bound = 1;
   std::vector<rt_material> materials;
   std::vector<uint8_t> texels;
   std::vector<rt_texture> tex_desc;
@@ -76,6 +80,7 @@ struct Scene {
 // fatal errors), prints the reference's warnings for skipped entries.
 std::unique_ptr<Scene> load_scene(const std::string& path, const std::string& texture_root, int res_w, int res_h);
 void build_bvh(Scene& sc);
+void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<int>& ref_leaf_of);
 rt_camera_desc camera_desc(const CameraDesc& c);
 rt_scene_desc scene_desc(const Scene& sc);
 M4 build_o2w(const V3& t, const V3& r, const V3& s, M4* w2o);
