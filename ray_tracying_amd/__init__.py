@@ -23,7 +23,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_DIR = os.path.join(_HERE, "lib")
+# RT_LIB_DIR overrides the library directory (A/B builds of the same sources); default in-tree
+LIB_DIR = os.environ.get("RT_LIB_DIR") or os.path.join(_HERE, "lib")
 
 __all__ = [
     "Scene", "RenderParams", "RenderStats", "quantise", "write_ppm", "make_soup",

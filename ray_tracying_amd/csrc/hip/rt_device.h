@@ -93,7 +93,7 @@ struct HitAttr {
 };
 
 // ---- Sphere::intersect (shapes.cpp:200-262): unit sphere in object space, motion blur
-template <bool kAttr>
+template <bool kAttr, bool kUV = true>
 __device__ __forceinline__ bool sphere_hit(const PrimA& P, const float4* rec, const Ray& ray,
                                            float& t_out, HitAttr* at) {
   V3 vel{P.a[12], P.a[13], P.a[14]};
@@ -119,10 +119,15 @@ __device__ __forceinline__ bool sphere_hit(const PrimA& P, const float4* rec, co
   if (kAttr) {
     at->p = hp;
     at->n = xnormal(P.a, pl);
-    const float PI = 3.1415926535f;
-    // double atan2/asin as in the reference; ocml, not glibc: UVs only feed textures.
-    at->u = (float)(0.5 + atan2((double)pl.z, (double)pl.x) / (double)(2.0f * PI));
-    at->v = (float)(0.5 - asin((double)pl.y) / (double)PI);
+    if (kUV) {
+      const float PI = 3.1415926535f;
+      // double atan2/asin as in the reference; ocml, not glibc: UVs only feed textures.
+      at->u = (float)(0.5 + atan2((double)pl.z, (double)pl.x) / (double)(2.0f * PI));
+      at->v = (float)(0.5 - asin((double)pl.y) / (double)PI);
+    } else {
+      at->u = 0.0f;
+      at->v = 0.0f;
+    }
   }
   return true;
 }
@@ -232,14 +237,15 @@ __device__ __forceinline__ bool plane_hit(const PrimA& P, const Ray& ray, float&
   return true;
 }
 
-template <bool kAttr>
+template <bool kAttr, bool kPlanesOnly = false, bool kUV = true>
 __device__ __forceinline__ bool prim_hit(const PrimA& P, const float4* rec, const Ray& ray,
                                          float& t, HitAttr* at) {
+  if (kPlanesOnly) return plane_hit<kAttr>(P, ray, t, at);
   switch (RT_TAG_KIND(prim_tag(P))) {
     case RT_PRIM_PLANE: return plane_hit<kAttr>(P, ray, t, at);
     case RT_PRIM_CUBE: return cube_hit<kAttr>(P, rec, ray, t, at);
     case RT_PRIM_RECTANGLE: return rect_hit<kAttr>(P, rec, ray, t, at);
-    default: return sphere_hit<kAttr>(P, rec, ray, t, at);
+    default: return sphere_hit<kAttr, kUV>(P, rec, ray, t, at);
   }
 }
 

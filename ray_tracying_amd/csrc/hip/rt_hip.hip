@@ -40,7 +40,8 @@ namespace {
 
 constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
 constexpr int kBlock = 256;
-constexpr int kLdsStack = 16;  // traversal stack entries per lane held in LDS (rest spill to HBM)
+constexpr int kLdsStack = 16;
+constexpr int kBatchShards = 32;  // sharded work counters: no hot atomic word  // traversal stack entries per lane held in LDS (rest spill to HBM)
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
@@ -92,7 +93,7 @@ struct LogicArgs {
   int n_pixels;  // n_tiles * tile_w * tile_h (launch-local pixel space)
   int n_samples; // s*s (1 when s <= 1)
   long long n_units;  // n_pixels * n_samples
-  unsigned long long* next_unit;
+  unsigned int* batch_ctr;  // kBatchShards counters; wave w pulls batches from counter w % kBatchShards
   float* samples;  // [n_units][3] per-sample Trace colours
   float* out;
   // buffers
@@ -102,8 +103,7 @@ struct LogicArgs {
   float* refr;           // [kMaxDepth][6][n_slots] (null if no refraction)
   float* query;          // [Q_COUNT][n_slots]
   const int* result;     // [n_slots]
-  int* qlist;            // compact list of slots with a pending query
-  unsigned int* qcount;
+  unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
 };
 
 struct TraceArgs {
@@ -114,9 +114,8 @@ struct TraceArgs {
   int n_nodes;
   const float* query;
   int* result;
-  const int* qlist;
-  const unsigned int* qcount;
-  unsigned int* fetch;        // persistent work counter (zeroed per launch)
+  unsigned int* fetch;        // persistent work counter over slots (zeroed per launch)
+  unsigned long long* rays;   // queries traced (one atomic per wave at exit)
   int n_slots;
   int lds_entries;            // traversal stack entries kept in LDS per lane
   int* spill;                 // deeper entries: [entry - lds_entries][n_threads]
@@ -142,7 +141,7 @@ __device__ __forceinline__ bool ref_leaf_ok(const TraceArgs& a, int leaf, const 
   return aabb_exact(blo, bhi, r, par, tn);
 }
 
-template <bool kCount>
+template <bool kCount, bool kPlanesOnly>
 __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cnt, const Ray& r, bool any, float tmax,
                                            uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
   for (int k = 0; k < cnt; ++k) {
@@ -152,7 +151,7 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
     load_prim_a(rec, P);
     float t;
     if (kCount) ++nprim;
-    if (!prim_hit<false>(P, rec, r, t, nullptr)) continue;
+    if (!prim_hit<false, kPlanesOnly>(P, rec, r, t, nullptr)) continue;
     const int2 ref = a.prim_refs[pi];
     if (any) {  // occluder iff t <= light_dist (raytracer.cpp:233)
       if (!(t > tmax) && (!check_leaf || ref_leaf_ok(a, ref.y, r, par))) {
@@ -178,11 +177,12 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
   ca = c;
 }
 
-template <bool kCount>
+template <bool kCount, bool kPlanesOnly>
 __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
-  const unsigned int nq = *ta.qcount;
+  const unsigned int nq = (unsigned)ta.n_slots;
   const int lane = threadIdx.x & 63;
+  unsigned int nrays = 0;
   const int gtid = blockIdx.x * kBlock + threadIdx.x;
   unsigned int nbox = 0, nprim = 0;
   const TraceArgs& a = ta;
@@ -194,12 +194,14 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
     if (base >= nq) break;
     const unsigned int qi = base + lane;
     if (qi >= nq) continue;
-    const int slot = ta.qlist[qi];
+    const int slot = (int)qi;
+    const int kind = __float_as_int(ta.query[Q_KIND * N + slot]);
+    if (kind < 0) continue;  // no query from this slot in this step
+    ++nrays;
     Ray r;
     r.o = V3{ta.query[(Q_O + 0) * N + slot], ta.query[(Q_O + 1) * N + slot], ta.query[(Q_O + 2) * N + slot]};
     r.d = V3{ta.query[(Q_D + 0) * N + slot], ta.query[(Q_D + 1) * N + slot], ta.query[(Q_D + 2) * N + slot]};
     const float tq = ta.query[Q_TMAX * N + slot];
-    const int kind = __float_as_int(ta.query[Q_KIND * N + slot]);
     const bool any = (kind & 1) != 0;
     const float tmax = any ? tq : 0.0f;
     r.time = any ? 0.0f : tq;  // shadow rays have time 0 (raytracer.cpp:225, shapes.hpp:28)
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
     par |= ((double)fabsf(r.d.y) < 1e-6) ? 2u : 0u;
     par |= ((double)fabsf(r.d.z) < 1e-6) ? 4u : 0u;
     if (a.c.n_prims > 0 && !a.c.use_bvh) {  // BVH::intersect_linear (acceleration.cpp:124-139)
-      test_prims<kCount>(a, 0, a.c.n_prims, r, any, tmax, par, false, h, nprim);
+      test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, r, any, tmax, par, false, h, nprim);
     } else if (a.c.n_prims > 0) {
       auto safe_inv = [](float d) {
         float dd = fabsf(d) < 1e-12f ? copysignf(1e-12f, d) : d;
@@ -249,7 +251,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
           if (hit[k] && (m & 0x80u)) {
             float lim = any ? tmax : h.best_t;
             lim = lim + (lim * 1e-5f + a.c.eps_abs);
-            if (!(tn[k] > lim)) test_prims<kCount>(a, cc[k], (int)(m & 0x7fu), r, any, tmax, par, true, h, nprim);
+            if (!(tn[k] > lim)) test_prims<kCount, kPlanesOnly>(a, cc[k], (int)(m & 0x7fu), r, any, tmax, par, true, h, nprim);
             hit[k] = false;
           }
         }
@@ -287,10 +289,13 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
       }
       // primitives whose accepted region is not boxable: tested by every ray
       if (!h.done && a.n_unbounded > 0)
-        test_prims<kCount>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, any, tmax, par, true, h, nprim);
+        test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, any, tmax, par, true, h, nprim);
     }
     ta.result[slot] = any ? (h.done ? 1 : 0) : h.best_idx;
   }
+  unsigned long long nr = nrays;
+  for (int off = 32; off > 0; off >>= 1) nr += __shfl_xor(nr, off);
+  if (lane == 0 && nr) atomicAdd(ta.rays, nr);
   if (kCount) {
     unsigned long long b = nbox, p = nprim;
     for (int off = 32; off > 0; off >>= 1) {
@@ -378,7 +383,14 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
   return pixel_coords(a, p, px, py, off);
 }
 
-__global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
+// kFrames: some material reflects or refracts (Trace recursion frames needed)
+// kTex: some material has a texture (hit UVs + texel fetch)
+// kPlanes: every primitive is a Plane (no transformed-shape intersection code)
+#ifndef RT_LOGIC_WAVES
+#define RT_LOGIC_WAVES 1
+#endif
+template <bool kFrames, bool kTex, bool kPlanes>
+__global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
   bool want = false;
   if (slot < a.n_slots) {
@@ -389,8 +401,8 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
     auto stu = [&](int f, uint32_t v) { S[f * N + slot] = v; };
     auto stf = [&](int f, float v) { S[f * N + slot] = __float_as_uint(v); };
 
-    long long unit = (long long)(int)ld(F_UNIT);
-    if (unit >= 0) {
+    long long unit = (long long)(int)ld(F_UNIT);  // >= 0 active, -2 idle (batch done), -1 retired
+    if (unit != -1) {
       const int s = a.spp_sqrt;
       uint32_t ctrl = ld(F_CTRL);
       int st = (int)(ctrl & 15u), depth = (int)(ctrl >> 4);
@@ -407,30 +419,42 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
       float hu = ldf(F_UV), hv = ldf(F_UV + 1);
       const int res = a.result[slot];
       int px = 0, py = 0, sample = 0;
-      bool inside = unit_coords(a, unit, px, py, sample);
+      bool inside = unit >= 0 && unit_coords(a, unit, px, py, sample);
       Rng rng;
       rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
       rng.ctr = ld(F_RNG);
       bool retired = false;
+      bool idle = unit == -2;
       V3 qo{0, 0, 0}, qd{0, 0, 0};
       float qtmax = 0.0f;
       int qkind = 0;
 
-      while (!want && !retired) {
+     for (int pass = 0; pass < 2; ++pass) {
+      if (pass == 1) {
+        // the whole wave finished its batch: pull the next 64 consecutive samples (one pixel's
+        // worth -> coherent rays) from this wave's counter shard
+        const int wave = (int)(slot >> 6);
+        const int shard = wave % kBatchShards;
+        const int leader = __ffsll((long long)__ballot(1)) - 1;  // lowest active lane
+        unsigned int j = 0;
+        if ((threadIdx.x & 63) == leader) j = atomicAdd(a.batch_ctr + shard, 1u);
+        j = __shfl(j, leader);
+        const long long batch = (long long)j * kBatchShards + shard;
+        unit = batch * 64 + (threadIdx.x & 63);
+        idle = false;
+        if (batch * 64 >= a.n_units || unit >= a.n_units) {
+          retired = true;
+        } else {
+          inside = unit_coords(a, unit, px, py, sample);
+          st = ST_SAMPLE;
+          if (!inside) idle = true;  // edge tile: pixel outside the image
+        }
+      }
+      while (!want && !retired && !idle) {
         V3 ret{0, 0, 0};
         bool returning = false;
         bool shade_now = false;
         if (st == ST_SAMPLE) {
-          if (!inside) {  // edge tile: skip units outside the image
-            for (;;) {
-              unsigned long long nu = atomicAdd(a.next_unit, 1ull);
-              if ((long long)nu >= a.n_units) { retired = true; break; }
-              unit = (long long)nu;
-              if (unit_coords(a, unit, px, py, sample)) break;
-            }
-            if (retired) break;
-            inside = true;
-          }
           // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)
           rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
           float fx, fy;
@@ -467,14 +491,14 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
             load_prim_a(rec, P);
             HitAttr at;
             float t;
-            prim_hit<true>(P, rec, ray, t, &at);  // bit-identical to the traversal's test
+            prim_hit<true, kPlanes, kTex>(P, rec, ray, t, &at);  // bit-identical to the traversal's test
             hp = at.p;
             hn = at.n;
             hu = at.u;
             hv = at.v;
             mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
             const rt_material& m = a.mats[mat_id];
-            V3 base = diffuse_color(a, m, hu, hv);
+            V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
             fin = V3{base.x * m.k_ambient, base.y * m.k_ambient, base.z * m.k_ambient};
             light = 0;
             ls = 0;
@@ -505,7 +529,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
             }
             vis = vis / (float)ns;
             if (!(vis <= 0.0f)) {
-              V3 base = diffuse_color(a, m, hu, hv);
+              V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
               V3 V = normalize(sub(ray.o, hp));
               V3 lc = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
               float dsq = dot(lc, lc);
@@ -535,7 +559,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
           Ray rr, tr;
           rr.time = 0.0f;
           tr.time = 0.0f;
-          if (m.reflectivity > 0.0f) {  // createReflectionRay (raytracer.cpp:101-115) + glossy fuzz
+          if (kFrames && m.reflectivity > 0.0f) {  // createReflectionRay (raytracer.cpp:101-115) + glossy fuzz
             float idn = dot(ray.d, hn);
             rr.d = sub(ray.d, mul(hn, 2.0f * idn));
             rr.o = add(hp, mul(hn, 1e-4f));
@@ -546,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
             }
             refl_ok = dot(rr.d, rr.d) > 0.001f;
           }
-          if (m.transparency > 0.0f) {  // createRefractionRay (raytracer.cpp:118-150)
+          if (kFrames && m.transparency > 0.0f) {  // createRefractionRay (raytracer.cpp:118-150)
             V3 N = hn;
             float n_in = 1.0f, n_out = m.refractive_index;
             float cos_i = dot(ray.d, N);
@@ -573,7 +597,7 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
           // a child that is not traced (invalid ray, or depth+1 > MAX) contributes (0,0,0)
           const bool refl_go = refl_ok && depth + 1 <= kMaxDepth;
           const bool refr_go = refr_ok && depth + 1 <= kMaxDepth;
-          if (!refl_go && !refr_go) {
+          if (!kFrames || (!refl_go && !refr_go)) {
             V3 part{A.x + m.reflectivity * 0.0f, A.y + m.reflectivity * 0.0f, A.z + m.reflectivity * 0.0f};
             ret = V3{part.x + m.transparency * 0.0f, part.y + m.transparency * 0.0f, part.z + m.transparency * 0.0f};
             returning = true;
@@ -615,16 +639,11 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
             a.samples[unit * 3 + 0] = ret.x;
             a.samples[unit * 3 + 1] = ret.y;
             a.samples[unit * 3 + 2] = ret.z;
-            unsigned long long nu = atomicAdd(a.next_unit, 1ull);
-            if ((long long)nu >= a.n_units) {
-              retired = true;
-            } else {
-              unit = (long long)nu;
-              inside = unit_coords(a, unit, px, py, sample);
-              st = ST_SAMPLE;
-            }
+            idle = true;  // wait for the rest of the wave's batch
+            unit = -2;
             break;
           }
+          if (!kFrames) break;  // unreachable: without frames every Trace returns at depth 0
           --depth;
           const uint32_t* F = a.frames + (size_t)depth * FR_COUNT * N;
           uint32_t meta = F[FR_META * N + slot];
@@ -658,8 +677,15 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
           }
         }
       }
+      // pass 2 only when no lane of the wave has a query and the wave is not finished
+      if (__ballot(want || (!idle && !retired)) != 0ull || __ballot(!retired) == 0ull) break;
+     }
       if (retired) {
         stu(F_UNIT, 0xFFFFFFFFu);
+        a.query[Q_KIND * N + slot] = __int_as_float(-1);
+      } else if (!want) {  // idle: keep the state, no query this step
+        stu(F_UNIT, (uint32_t)-2);
+        a.query[Q_KIND * N + slot] = __int_as_float(-1);
       } else {
         stu(F_UNIT, (uint32_t)unit);
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
@@ -683,16 +709,8 @@ __global__ __launch_bounds__(kBlock) void logic_kernel(LogicArgs a) {
       }
     }
   }
-  // append slots with a query to the compact list: one atomic per wave
-  const unsigned long long m = __ballot(want);
-  if (m) {
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)m) - 1;
-    unsigned int base = 0;
-    if (lane == leader) base = atomicAdd(a.qcount, (unsigned int)__popcll(m));
-    base = __shfl(base, leader);
-    if (want) a.qlist[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
-  }
+  // tell the host another step is needed: a plain store, no atomic (all writers store 1)
+  if (__ballot(want) != 0ull && (threadIdx.x & 63) == 0) *a.any_query = 1u;
 }
 
 // compute_pixel_color's accumulation (raytracer.cpp:46-69): totalColor starts at {0,0,0},
@@ -721,13 +739,30 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
 
 // slot initialisation: slot k takes unit k (units past the end retire immediately); a unit
 // whose pixel is outside the image (edge tiles) is skipped by the first logic step.
-__global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, long long n_units, int* result) {
+__global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, long long n_units, int* result,
+                                                      float* query) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
   if (slot >= n_slots) return;
   for (int f = 0; f < F_COUNT; ++f) state[f * n_slots + slot] = 0u;
-  state[F_UNIT * n_slots + slot] = (long long)slot < n_units ? (uint32_t)slot : 0xFFFFFFFFu;
+  state[F_UNIT * n_slots + slot] = (uint32_t)-2;  // idle: the first logic step pulls a batch
   state[F_CTRL * n_slots + slot] = ST_SAMPLE;
   result[slot] = -1;
+  query[Q_KIND * n_slots + slot] = __int_as_float(-1);
+}
+
+template <bool F, bool T>
+void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_t st) {
+  if (planes) hipLaunchKernelGGL((logic_kernel<F, T, true>), dim3(blocks), dim3(kBlock), 0, st, la);
+  else hipLaunchKernelGGL((logic_kernel<F, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
+}
+void launch_logic(const LogicArgs& la, bool frames, bool tex, bool planes, unsigned blocks, hipStream_t st) {
+  if (frames) {
+    if (tex) launch_logic2<true, true>(la, planes, blocks, st);
+    else launch_logic2<true, false>(la, planes, blocks, st);
+  } else {
+    if (tex) launch_logic2<false, true>(la, planes, blocks, st);
+    else launch_logic2<false, false>(la, planes, blocks, st);
+  }
 }
 
 // ---------------------------------------------------------------- C ABI support
@@ -767,7 +802,8 @@ struct rt_scene_s {
   int* d_spill = nullptr;
   size_t spill_cap = 0;
   // per-render workspace (grown on demand)
-  void* d_ctl = nullptr;  // bytes 0: qcount (u32), 4: trace fetch (u32), 8: next_unit (u64), 16/24: box/prim (u64)
+  void* d_ctl = nullptr;  // bytes 0: any_query (u32), 4: trace fetch (u32), 16/24: box/prim tests, 32: rays (u64),
+                          // 256: batch counter shards (kBatchShards x u32)
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
   uint32_t* d_state = nullptr;
@@ -777,19 +813,17 @@ struct rt_scene_s {
   float* d_samples = nullptr;
   size_t samples_cap = 0;
   int* d_result = nullptr;
-  int* d_qlist = nullptr;
   size_t slots_cap = 0;
-  unsigned int* h_qcount = nullptr;  // pinned
-  unsigned long long h_ctl_init = 0;
+  unsigned int* h_flag = nullptr;  // pinned
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_a = nullptr, ev_b = nullptr;
 };
 
 static void free_workspace(rt_scene_s* s) {
-  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_qlist, s->d_samples};
+  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
-  s->d_query = nullptr; s->d_result = nullptr; s->d_qlist = nullptr; s->d_samples = nullptr;
+  s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr;
   s->slots_cap = 0;
   s->samples_cap = 0;
 }
@@ -832,7 +866,7 @@ int rt_scene_destroy(rt_scene_t s) {
                   s->d_prim_refs, s->d_ref_boxes, s->d_spill};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  if (s->h_qcount) (void)hipHostFree(s->h_qcount);
+  if (s->h_flag) (void)hipHostFree(s->h_flag);
   hipEvent_t evs[] = {s->ev_t0, s->ev_t1, s->ev_a, s->ev_b};
   for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
@@ -870,7 +904,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     rt_scene_destroy(s);
     return rc;
   }
-  if (hipMalloc(&s->d_ctl, 64) != hipSuccess || hipHostMalloc((void**)&s->h_qcount, 64) != hipSuccess ||
+  if (hipMalloc(&s->d_ctl, 1024) != hipSuccess || hipHostMalloc((void**)&s->h_flag, 64) != hipSuccess ||
       hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
       hipEventCreate(&s->ev_a) != hipSuccess || hipEventCreate(&s->ev_b) != hipSuccess) {
     rt_scene_destroy(s);
@@ -880,7 +914,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const int lds_entries = std::min(d->stack_bound, kLdsStack);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<false>, kBlock,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (d->prim_stride == 64 ? trace_kernel<false, true> : trace_kernel<false, false>), kBlock,
                                                      (size_t)lds_entries * kBlock * sizeof(int)) != hipSuccess || bpc < 1)
       bpc = 2;
     s->n_cu = ncu;
@@ -915,9 +949,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // ---- workspace
   const bool need_frames = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
   const bool need_refr = (s->desc.flags & RT_SCENE_HAS_REFRACTION) != 0;
+  const bool planes_only = s->desc.prim_stride == 64;
   const int n_samples = p->spp_sqrt <= 1 ? 1 : p->spp_sqrt * p->spp_sqrt;
   const long long n_units = (long long)n_pixels * n_samples;
-  const int n_slots = (int)std::min<long long>(n_units, 1 << 20);
+  // whole blocks of slots; a wave renders 64 consecutive samples per batch
+  const int n_slots = (int)(((std::min<long long>(n_units, 1 << 20) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     s->d_tiles = nullptr;
@@ -931,7 +967,6 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_state, N * F_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_qlist, N * 4), RT_ENOMEM);
     if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
     if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
     s->slots_cap = N;
@@ -945,9 +980,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   }
   HIP_TRY(hipMemcpyAsync(s->d_tiles, tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream), RT_EDEVICE);
   unsigned int* ctl = (unsigned int*)s->d_ctl;
-  HIP_TRY(hipMemsetAsync(ctl, 0, 64, stream), RT_EDEVICE);
-  s->h_ctl_init = (unsigned long long)n_slots;
-  HIP_TRY(hipMemcpyAsync(ctl + 2, &s->h_ctl_init, 8, hipMemcpyHostToDevice, stream), RT_EDEVICE);
+  HIP_TRY(hipMemsetAsync(ctl, 0, 1024, stream), RT_EDEVICE);
 
   LogicArgs la{};
   Common c{};
@@ -975,7 +1008,6 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.n_pixels = n_pixels;
   la.n_samples = n_samples;
   la.n_units = n_units;
-  la.next_unit = (unsigned long long*)(ctl + 2);
   la.samples = s->d_samples;
   la.out = d_out;
   la.n_slots = n_slots;
@@ -984,8 +1016,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.refr = s->d_refr;
   la.query = s->d_query;
   la.result = s->d_result;
-  la.qlist = s->d_qlist;
-  la.qcount = ctl;
+  la.any_query = ctl;
+  la.batch_ctr = ctl + 64;  // byte 256
 
   TraceArgs ta{};
   ta.c = c;
@@ -995,9 +1027,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.n_nodes = s->desc.n_nodes;
   ta.query = s->d_query;
   ta.result = s->d_result;
-  ta.qlist = s->d_qlist;
-  ta.qcount = ctl;
   ta.fetch = ctl + 1;
+  ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
   ta.lds_entries = std::min(s->desc.stack_bound, kLdsStack);
   const unsigned trace_blocks = (unsigned)std::max(1, std::min(s->n_cu * s->trace_blocks_per_cu,
@@ -1016,45 +1047,49 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const size_t lds = (size_t)ta.lds_entries * kBlock * sizeof(int);
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result);
+  hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result,
+                     s->d_query);
   HIP_TRY(hipGetLastError(), RT_EDEVICE);
 
   // ---- iterate logic -> trace until no slot issues a query
-  uint64_t rays = 0;
   double trace_ms = 0.0;
   int iters = 0;
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
   for (;;) {
-    HIP_TRY(hipMemsetAsync(ctl, 0, 8, stream), RT_EDEVICE);  // qcount + trace fetch counter
-    hipLaunchKernelGGL(logic_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, la);
+    HIP_TRY(hipMemsetAsync(ctl, 0, 8, stream), RT_EDEVICE);  // any_query + trace fetch counter
+    launch_logic(la, need_frames, (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0, planes_only, slot_blocks, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipMemcpyAsync(s->h_qcount, ctl, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipMemcpyAsync(s->h_flag, ctl, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
-    if (p->count_work)
-      hipLaunchKernelGGL(trace_kernel<true>, dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
-    else
-      hipLaunchKernelGGL(trace_kernel<false>, dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+    if (p->count_work) {
+      if (planes_only) hipLaunchKernelGGL((trace_kernel<true, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+      else hipLaunchKernelGGL((trace_kernel<true, false>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+    } else {
+      if (planes_only) hipLaunchKernelGGL((trace_kernel<false, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+      else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+    }
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
     HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
-    unsigned int nq = *s->h_qcount;
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev_a, s->ev_b), RT_EDEVICE);
-    trace_ms += ms;
-    rays += nq;
-    ++iters;
-    if (nq == 0) break;
+    const bool more = *s->h_flag != 0;
+    if (more) {  // the final (empty) trace launch is not a traversal step
+      trace_ms += ms;
+      ++iters;
+    }
+    if (!more) break;
   }
   hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
   HIP_TRY(hipGetLastError(), RT_EDEVICE);
   HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
   HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
   if (stats) {
-    unsigned long long cnt[2] = {0, 0};
+    unsigned long long cnt[3] = {0, 0, 0};
     HIP_TRY(hipMemcpy(cnt, ctl + 4, sizeof(cnt), hipMemcpyDeviceToHost), RT_EDEVICE);
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1), RT_EDEVICE);
-    stats->rays = rays;
+    stats->rays = cnt[2];
     stats->box_tests = cnt[0];
     stats->prim_tests = cnt[1];
     stats->kernel_ms = ms;
