@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -244,16 +245,25 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
         }
         if (kCount) nbox += __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
                                                 (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
-        // leaves first (their hits tighten the bound before internal children are ordered)
+        // leaves first (their hits tighten the bound before internal children are ordered);
+        // one primitive-test instance walks the leaf bitmask (no 4x inlined copies)
+        uint32_t leaves = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint32_t m = (meta >> (8 * k)) & 0xffu;
-          if (hit[k] && (m & 0x80u)) {
-            float lim = any ? tmax : h.best_t;
-            lim = lim + (lim * 1e-5f + a.c.eps_abs);
-            if (!(tn[k] > lim)) test_prims<kCount, kPlanesOnly>(a, cc[k], (int)(m & 0x7fu), r, any, tmax, par, true, h, nprim);
+          if (hit[k] && ((meta >> (8 * k)) & 0x80u)) {
+            leaves |= 1u << k;
             hit[k] = false;
           }
+        }
+        while (leaves != 0u) {
+          const int k = __builtin_ctz(leaves);
+          leaves &= leaves - 1u;
+          const float tk = k == 0 ? tn[0] : k == 1 ? tn[1] : k == 2 ? tn[2] : tn[3];
+          const int ck = k == 0 ? cc[0] : k == 1 ? cc[1] : k == 2 ? cc[2] : cc[3];
+          float lim = any ? tmax : h.best_t;
+          lim = lim + (lim * 1e-5f + a.c.eps_abs);
+          if (!(tk > lim)) test_prims<kCount, kPlanesOnly>(a, ck, (int)((meta >> (8 * k)) & 0x7fu), r, any, tmax, par, true, h, nprim);
+          if (h.done) break;
         }
         if (h.done) break;
         float lim = any ? tmax : h.best_t;
@@ -953,7 +963,9 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const int n_samples = p->spp_sqrt <= 1 ? 1 : p->spp_sqrt * p->spp_sqrt;
   const long long n_units = (long long)n_pixels * n_samples;
   // whole blocks of slots; a wave renders 64 consecutive samples per batch
-  const int n_slots = (int)(((std::min<long long>(n_units, 1 << 20) + kBlock - 1) / kBlock) * kBlock);
+  long long slot_cap = 1 << 23;  // 8M slots: ~16 fetches per trace wave per launch (measured best; 1M: -28%)
+  if (const char* e = std::getenv("RT_SLOTS")) slot_cap = std::max(1LL << 12, std::atoll(e));
+  const int n_slots = (int)(((std::min<long long>(n_units, slot_cap) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     s->d_tiles = nullptr;
