@@ -61,18 +61,28 @@ typedef struct rt_prim {
   float b[16];
 } rt_prim;
 
-/* Traversal node: 4-wide, 128 bytes (one cache line), children's boxes in SoA order.
- * Built on the host with binned SAH over conservative per-primitive hit boxes
- * (bvh_wide.cpp); the reference's own median-split tree (acceleration.cpp:20-64) is NOT used
- * for traversal -- its leaves survive as rt_prim_ref.ref_leaf / ref_leaf_boxes, the exact
- * filter every candidate hit must pass (AABB::intersect, shapes.cpp:55-72).
+/* Traversal node: 4-wide, 64 bytes (half a cache line).  Built on the host with binned SAH
+ * over conservative per-primitive hit boxes (bvh_wide.cpp); the reference's own median-split
+ * tree (acceleration.cpp:20-64) is NOT used for traversal -- its leaves survive as
+ * rt_prim_ref.ref_leaf / ref_leaf_boxes, the exact filter every candidate hit must pass
+ * (AABB::intersect, shapes.cpp:55-72).
+ * Child boxes are 8-bit coordinates on a per-node grid: bound = origin[a] + q * 2^(e[a]-127).
+ * The host picks every q so that this value is <= the child's lo (resp. >= its hi): the grid
+ * box always contains the full-precision one, so culling stays conservative.  The kernel
+ * evaluates the slab as fma(q, 2^k * inv, (origin - o) * inv) -- rounding of the same order
+ * as the plain (lo - o) * inv form, far inside the boxes' 1e-5 * scale padding.
+ *   exps: e_x | e_y << 8 | e_z << 16 (biased binary32 exponents of the grid steps)
+ *   q_lo_x: byte k = child k's lo.x code (likewise q_hi_x .. q_hi_z)
  *   meta byte k: 0 = no child; 0x01 = internal child (child[k] = node index);
  *                0x80 | n = leaf child with n primitives starting at child[k]. */
 typedef struct rt_node4 {
-  float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
-  int32_t child[4];
+  float origin[3];
+  uint32_t exps;
+  uint32_t q_lo_x, q_hi_x, q_lo_y, q_hi_y;
+  uint32_t q_lo_z, q_hi_z;
   uint32_t meta;
-  uint32_t pad[3];
+  int32_t child[4];
+  uint32_t pad;
 } rt_node4;
 
 /* Per primitive (in traversal order): its position in the reference's BVH-sorted list

@@ -125,6 +125,7 @@ struct TraceArgs {
 };
 
 // ---------------------------------------------------------------- traversal
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 // The closest-hit / any-hit state of one query.
 struct HitState {
   float best_t;
@@ -223,23 +224,39 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
       int sp = 0;
       int node = a.n_nodes > 0 ? 0 : -1;
       while (node >= 0) {
-        const float4* nd = a.c.nodes + (size_t)node * 8;
-        const float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5];
-        const int4 ch = *reinterpret_cast<const int4*>(nd + 6);
-        const uint32_t meta = *reinterpret_cast<const uint32_t*>(nd + 7);
-        const float clx[4] = {lx.x, lx.y, lx.z, lx.w}, chx[4] = {hx.x, hx.y, hx.z, hx.w};
-        const float cly[4] = {ly.x, ly.y, ly.z, ly.w}, chy[4] = {hy.x, hy.y, hy.z, hy.w};
-        const float clz[4] = {lz.x, lz.y, lz.z, lz.w}, chz[4] = {hz.x, hz.y, hz.z, hz.w};
-        const int cc[4] = {ch.x, ch.y, ch.z, ch.w};
+        // 64-B node, 8-bit child grids (rt_hip.h).  Slab entry/exit along x for child k:
+        // (origin + q*step - o) * inv == q * (step*inv) + (origin - o)*inv, evaluated as one
+        // packed fma per pair of children: culling only -- the boxes carry 1e-5*scale padding
+        // and every candidate hit is re-checked exactly (ref_leaf_ok + the primitive test).
+        const float4* nd = a.c.nodes + (size_t)node * 4;
+        const float4 g = nd[0];
+        const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
+        const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
+        const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
+        const uint32_t ex = __float_as_uint(g.w);
+        const uint32_t meta = qb.z;
+        const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
+        const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
+        const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
+        const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
+        const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
+        auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
+        auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };
+        const f32x2 t_lx01 = __builtin_elementwise_fma(lo2(qa.x), Bx, Ax), t_lx23 = __builtin_elementwise_fma(hi2(qa.x), Bx, Ax);
+        const f32x2 t_hx01 = __builtin_elementwise_fma(lo2(qa.y), Bx, Ax), t_hx23 = __builtin_elementwise_fma(hi2(qa.y), Bx, Ax);
+        const f32x2 t_ly01 = __builtin_elementwise_fma(lo2(qa.z), By, Ay), t_ly23 = __builtin_elementwise_fma(hi2(qa.z), By, Ay);
+        const f32x2 t_hy01 = __builtin_elementwise_fma(lo2(qa.w), By, Ay), t_hy23 = __builtin_elementwise_fma(hi2(qa.w), By, Ay);
+        const f32x2 t_lz01 = __builtin_elementwise_fma(lo2(qb.x), Bz, Az), t_lz23 = __builtin_elementwise_fma(hi2(qb.x), Bz, Az);
+        const f32x2 t_hz01 = __builtin_elementwise_fma(lo2(qb.y), Bz, Az), t_hz23 = __builtin_elementwise_fma(hi2(qb.y), Bz, Az);
+        const float tx1[4] = {t_lx01.x, t_lx01.y, t_lx23.x, t_lx23.y}, tx2[4] = {t_hx01.x, t_hx01.y, t_hx23.x, t_hx23.y};
+        const float ty1[4] = {t_ly01.x, t_ly01.y, t_ly23.x, t_ly23.y}, ty2[4] = {t_hy01.x, t_hy01.y, t_hy23.x, t_hy23.y};
+        const float tz1[4] = {t_lz01.x, t_lz01.y, t_lz23.x, t_lz23.y}, tz2[4] = {t_hz01.x, t_hz01.y, t_hz23.x, t_hz23.y};
         float tn[4];
         bool hit[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float tx1 = (clx[k] - r.o.x) * inv.x, tx2 = (chx[k] - r.o.x) * inv.x;
-          const float ty1 = (cly[k] - r.o.y) * inv.y, ty2 = (chy[k] - r.o.y) * inv.y;
-          const float tz1 = (clz[k] - r.o.z) * inv.z, tz2 = (chz[k] - r.o.z) * inv.z;
-          const float n0 = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-          const float f0 = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+          const float n0 = fmaxf(fmaxf(fminf(tx1[k], tx2[k]), fminf(ty1[k], ty2[k])), fminf(tz1[k], tz2[k]));
+          const float f0 = fminf(fminf(fmaxf(tx1[k], tx2[k]), fmaxf(ty1[k], ty2[k])), fmaxf(tz1[k], tz2[k]));
           tn[k] = n0;
           hit[k] = ((meta >> (8 * k)) & 0xffu) != 0 && n0 <= f0 && f0 >= 0.0f;
         }

@@ -1,5 +1,5 @@
 // bvh_wide.cpp -- traversal BVH for the MI355X kernel: binned-SAH BVH2 collapsed to 4-wide
-// nodes (rt_node4, 128 B = one cache line), built over conservative per-primitive HIT boxes.
+// nodes (rt_node4, 64 B, 8-bit conservative child grids), built over conservative per-primitive HIT boxes.
 //
 // Exactness contract: the reference accepts a primitive hit only
 // if the primitive's leaf box in the REFERENCE's median-split tree passes the exact slab test
@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <stdexcept>
 #include <vector>
 
 #include "scene.hpp"
@@ -192,6 +193,65 @@ bool tri_region(const double A[3], const double B[3], const double C[3], const d
 
 }  // namespace
 
+// Grid coordinate origin + q * step as a real number (double: exact for the 8-bit code and a
+// power-of-two step unless the exponents are ~29 apart, and then off by < 2^-53 relative).
+// The trace kernel never rounds this value: it folds it into the slab as
+// fma(q, step * inv, (origin - o) * inv) (rt_hip.hip), whose rounding, like the plain
+// slab form's, is orders of magnitude inside the 1e-5 * scale box padding.
+static inline double grid_value(float origin, uint32_t q, float step) { return (double)origin + (double)q * (double)step; }
+
+// Per-axis 8-bit grid codes for the first n child boxes of `out` (rt_hip.h, rt_node4): every
+// grid lo is <= the box's lo and every grid hi >= its hi.
+// Unused slots get an empty box (lo code 255, hi code 0; their meta byte is 0 anyway).
+static void quantise_children(rt_node4& out, const Box* cb, int n) {
+  uint32_t qlo[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, qhi[3] = {0, 0, 0};
+  uint32_t exps = 0;
+  for (int a = 0; a < 3; ++a) {
+    float lo = cb[0].lo[a], hi = cb[0].hi[a];
+    for (int k = 1; k < n; ++k) {
+      lo = std::min(lo, cb[k].lo[a]);
+      hi = std::max(hi, cb[k].hi[a]);
+    }
+    const float origin = lo;
+    // smallest power-of-two step whose 255 steps span the extent; grown until every
+    // child bound is representable conservatively
+    const double ext = (double)hi - (double)lo;
+    int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -126;
+    e = std::max(e, -126);
+    uint32_t codes_lo = 0, codes_hi = 0;
+    for (;; ++e) {
+      if (e > 80) throw std::runtime_error("BVH node grid: scene extent too large (> 2^88)");
+      const float step = std::ldexp(1.0f, e);
+      bool ok = true;
+      codes_lo = codes_hi = 0;
+      for (int k = 0; k < 4 && ok; ++k) {
+        uint32_t ql = 255, qh = 0;
+        if (k < n) {
+          const double fl = std::floor(((double)cb[k].lo[a] - (double)origin) / (double)step);
+          ql = (uint32_t)std::max(0.0, std::min(255.0, fl));
+          while (ql > 0 && grid_value(origin, ql, step) > cb[k].lo[a]) --ql;
+          if (grid_value(origin, ql, step) > cb[k].lo[a]) ok = false;
+          const double ch = std::ceil(((double)cb[k].hi[a] - (double)origin) / (double)step);
+          qh = (uint32_t)std::max(0.0, std::min(255.0, ch));
+          while (qh < 255 && grid_value(origin, qh, step) < cb[k].hi[a]) ++qh;
+          if (grid_value(origin, qh, step) < cb[k].hi[a]) ok = false;
+        }
+        codes_lo |= ql << (8 * k);
+        codes_hi |= qh << (8 * k);
+      }
+      if (ok) break;
+    }
+    out.origin[a] = origin;
+    exps |= (uint32_t)(e + 127) << (8 * a);
+    qlo[a] = codes_lo;
+    qhi[a] = codes_hi;
+  }
+  out.exps = exps;
+  out.q_lo_x = qlo[0]; out.q_hi_x = qhi[0];
+  out.q_lo_y = qlo[1]; out.q_hi_y = qhi[1];
+  out.q_lo_z = qlo[2]; out.q_hi_z = qhi[2];
+}
+
 // Fills sc.node4 / sc.prims order / prim_refs / ref_leaf_boxes / n_unbounded.
 // `ref_order` = the reference's BVH-sorted shape order, `ref_leaf_of` = reference leaf id per
 // sorted position, `ref_leaf_boxes` = the exact reference leaf boxes.
@@ -299,16 +359,15 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
       }
       rt_node4 out{};
       uint32_t meta = 0;
+      Box cb[4];
+      int nk = 0;
       for (int k = 0; k < 4; ++k) {
         if (k >= (int)kids.size()) {
-          out.lo_x[k] = out.lo_y[k] = out.lo_z[k] = 1.0f;
-          out.hi_x[k] = out.hi_y[k] = out.hi_z[k] = -1.0f;
           out.child[k] = -1;
           continue;
         }
         const Node2& c = B.nodes[kids[k]];
-        out.lo_x[k] = c.box.lo[0]; out.lo_y[k] = c.box.lo[1]; out.lo_z[k] = c.box.lo[2];
-        out.hi_x[k] = c.box.hi[0]; out.hi_y[k] = c.box.hi[1]; out.hi_z[k] = c.box.hi[2];
+        cb[nk++] = c.box;
         if (c.left < 0) {
           out.child[k] = c.start;  // first primitive (new order == bounded order)
           meta |= (0x80u | (uint32_t)c.count) << (8 * k);
@@ -317,6 +376,7 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
           meta |= 0x01u << (8 * k);
         }
       }
+      quantise_children(out, cb, nk);
       out.meta = meta;
       sc.node4[it.slot] = out;
     }

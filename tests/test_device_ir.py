@@ -35,6 +35,9 @@ def test_no_approximate_div_sqrt(ir):
     assert "!fpmath" not in ir
 
 
-def test_fma_only_in_powf_double_path(ir):
-    # the only fused ops allowed are the f64 fma of the glibc powf restatement
+def test_fma_only_in_powf_and_culling(ir):
+    # fused ops allowed: the f64 fma of the glibc powf restatement, and the packed (v2f32)
+    # fma of the BVH slab test, which only culls (padded boxes, exact re-check of every
+    # candidate hit).  No scalar f32 fma anywhere a result is computed.
     assert "@llvm.fma.f32" not in ir
+    assert "@llvm.fma.v2f32" in ir  # the culling slab is where the packed form is expected
