@@ -10,13 +10,15 @@
 //                 its colour to the sample buffer and the slot pulls the next (pixel, sample)
 //                 unit from an atomic counter (64 consecutive units = 64 samples of one pixel:
 //                 maximally coherent rays per wave).
-//   reduce_kernel one thread per pixel: compute_pixel_color's sum over the s*s samples in
+//   reduce_kernel one thread per pixel (samples staged through LDS): compute_pixel_color sum over the s*s samples in
 //                 the reference's order, then the division (raytracer.cpp:46-69).
 //   trace_kernel  one thread per query.  BVH::get_intersection (acceleration.cpp:142):
 //                 closest-hit for camera/reflection/refraction rays, any-hit-within-tmax for
 //                 shadow rays (== the reference's `!hit.shape || t > light_dist`,
-//                 raytracer.cpp:233).  BVH2 nodes (64 B = both child boxes), near-first
-//                 with t-pruning, per-lane stack in LDS (lane-minor -> conflict-free).
+//                 raytracer.cpp:233).  Persistent waves of 64 consecutive slots (one pixel
+//                 batch: coherent rays), 4-wide BVH with 64-B nodes (8-bit conservative
+//                 child grids), leaves tested first, near-first order with t-pruning,
+//                 per-lane stack in LDS (lane-minor -> conflict-free) with HBM spill.
 //
 // Splitting them keeps the heavy recursion/shading state out of the traversal's registers
 // (fused, the allocator needed ~250 VGPRs = 1 wave/SIMD).  Leaf boxes are tested with the
@@ -179,8 +181,9 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
   ca = c;
 }
 
+// 5 waves/SIMD (96 VGPRs, a few spills outside the node loop) measured 2% faster than 4
 template <bool kCount, bool kPlanesOnly>
-__global__ __launch_bounds__(kBlock) void trace_kernel(TraceArgs ta) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void trace_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_slots;
   const int lane = threadIdx.x & 63;
@@ -743,19 +746,41 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
 // compute_pixel_color's accumulation (raytracer.cpp:46-69): totalColor starts at {0,0,0},
 // adds every sample's Trace colour in (j, i) order, then divides by (float)(s*s); with
 // s <= 1 the single Trace colour is returned as is.
+constexpr int kRedChunk = 16;                  // samples per pixel staged per pass
+constexpr int kRedStride = kRedChunk * 3 + 1;  // padded LDS row (odd: conflict-free column reads)
 __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
-  const int p = blockIdx.x * kBlock + threadIdx.x;
+  // The block's 256 pixels own a contiguous run of samples (unit = pixel * n_samples + s,
+  // 3 floats each).  Each pass stages 16 samples of every pixel through LDS with coalesced
+  // loads; every thread then adds its own pixel's samples in the reference's order.
+  __shared__ float stage[kBlock * kRedStride];
+  const int p0 = blockIdx.x * kBlock;
+  const int np = min(kBlock, a.n_pixels - p0);
+  const int p = p0 + (int)threadIdx.x;
+  const size_t row = (size_t)a.n_samples * 3;
+  const float* base = a.samples + (size_t)p0 * row;
+  V3 acc{0.0f, 0.0f, 0.0f};
+  const int ns = a.spp_sqrt <= 1 ? 1 : a.n_samples;
+  for (int s0 = 0; s0 < ns; s0 += kRedChunk) {
+    const int cw = min(kRedChunk, ns - s0) * 3;  // floats per pixel in this pass
+    for (int i = (int)threadIdx.x; i < np * cw; i += kBlock) {
+      const int j = i / cw, r = i - j * cw;
+      stage[j * kRedStride + r] = base[(size_t)j * row + (size_t)s0 * 3 + r];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      const float* q = stage + threadIdx.x * kRedStride;
+      if (a.spp_sqrt <= 1) acc = V3{q[0], q[1], q[2]};
+      else
+        for (int k = 0; k < cw; k += 3) acc = V3{acc.x + q[k], acc.y + q[k + 1], acc.z + q[k + 2]};
+    }
+    __syncthreads();
+  }
   if (p >= a.n_pixels) return;
   int x, y;
   size_t off;
   if (!pixel_coords(a, p, x, y, off)) return;
-  const float* smp = a.samples + (size_t)p * a.n_samples * 3;
-  V3 c;
-  if (a.spp_sqrt <= 1) {
-    c = V3{smp[0], smp[1], smp[2]};
-  } else {
-    V3 acc{0.0f, 0.0f, 0.0f};
-    for (int k = 0; k < a.n_samples; ++k) acc = V3{acc.x + smp[3 * k], acc.y + smp[3 * k + 1], acc.z + smp[3 * k + 2]};
+  V3 c = acc;
+  if (a.spp_sqrt > 1) {  // compute_pixel_color: sum / (float)(s*s) (raytracer.cpp:46-69)
     const float tot = (float)a.n_samples;
     c = V3{acc.x / tot, acc.y / tot, acc.z / tot};
   }
