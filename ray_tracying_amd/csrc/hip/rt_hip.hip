@@ -436,18 +436,39 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       const int s = a.spp_sqrt;
       uint32_t ctrl = ld(F_CTRL);
       int st = (int)(ctrl & 15u), depth = (int)(ctrl >> 4);
-      int light = (int)ld(F_LIGHT), ls = (int)ld(F_LS);
+      // Only what the entry state reads is loaded: a closest-hit result needs the ray that
+      // was traced (still in the query record); a shadow result needs the hit and the
+      // shade accumulators; a new sample needs nothing.
+      const int st0 = unit >= 0 ? st : -1;
+      int light = 0, ls = 0, mat_id = 0;
       Ray ray;
-      ray.o = V3{ldf(F_RAY), ldf(F_RAY + 1), ldf(F_RAY + 2)};
-      ray.d = V3{ldf(F_RAY + 3), ldf(F_RAY + 4), ldf(F_RAY + 5)};
-      ray.time = ldf(F_RAY + 6);
-      V3 hp{ldf(F_HP), ldf(F_HP + 1), ldf(F_HP + 2)};
-      V3 hn{ldf(F_HN), ldf(F_HN + 1), ldf(F_HN + 2)};
-      int mat_id = (int)ld(F_MAT);
-      float vis = ldf(F_VIS);
-      V3 fin{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
-      float hu = ldf(F_UV), hv = ldf(F_UV + 1);
-      const int res = a.result[slot];
+      ray.o = V3{0.0f, 0.0f, 0.0f};
+      ray.d = V3{0.0f, 0.0f, 0.0f};
+      ray.time = 0.0f;
+      V3 hp{0.0f, 0.0f, 0.0f}, hn{0.0f, 0.0f, 0.0f}, fin{0.0f, 0.0f, 0.0f};
+      float vis = 0.0f, hu = 0.0f, hv = 0.0f;
+      if (st0 == ST_SHADOW) {
+        light = (int)ld(F_LIGHT);
+        ls = (int)ld(F_LS);
+        ray.o = V3{ldf(F_RAY), ldf(F_RAY + 1), ldf(F_RAY + 2)};
+        ray.d = V3{ldf(F_RAY + 3), ldf(F_RAY + 4), ldf(F_RAY + 5)};
+        ray.time = ldf(F_RAY + 6);
+        hp = V3{ldf(F_HP), ldf(F_HP + 1), ldf(F_HP + 2)};
+        hn = V3{ldf(F_HN), ldf(F_HN + 1), ldf(F_HN + 2)};
+        mat_id = (int)ld(F_MAT);
+        vis = ldf(F_VIS);
+        fin = V3{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
+        if (kTex) {
+          hu = ldf(F_UV);
+          hv = ldf(F_UV + 1);
+        }
+      } else if (st0 == ST_CLOSEST) {
+        const float* Q = a.query;
+        ray.o = V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]};
+        ray.d = V3{Q[(Q_D + 0) * N + slot], Q[(Q_D + 1) * N + slot], Q[(Q_D + 2) * N + slot]};
+        ray.time = Q[Q_TMAX * N + slot];  // closest queries carry the ray time there
+      }
+      const int res = st0 >= ST_CLOSEST ? a.result[slot] : -1;
       int px = 0, py = 0, sample = 0;
       bool inside = unit >= 0 && unit_coords(a, unit, px, py, sample);
       Rng rng;
@@ -719,18 +740,25 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       } else {
         stu(F_UNIT, (uint32_t)unit);
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
-        stu(F_LIGHT, (uint32_t)light);
-        stu(F_LS, (uint32_t)ls);
         stu(F_RNG, rng.ctr);
-        stf(F_RAY, ray.o.x); stf(F_RAY + 1, ray.o.y); stf(F_RAY + 2, ray.o.z);
-        stf(F_RAY + 3, ray.d.x); stf(F_RAY + 4, ray.d.y); stf(F_RAY + 5, ray.d.z);
-        stf(F_RAY + 6, ray.time);
-        stf(F_HP, hp.x); stf(F_HP + 1, hp.y); stf(F_HP + 2, hp.z);
-        stf(F_HN, hn.x); stf(F_HN + 1, hn.y); stf(F_HN + 2, hn.z);
-        stu(F_MAT, (uint32_t)mat_id);
-        stf(F_VIS, vis);
-        stf(F_FIN, fin.x); stf(F_FIN + 1, fin.y); stf(F_FIN + 2, fin.z);
-        stf(F_UV, hu); stf(F_UV + 1, hv);
+        if (st == ST_SHADOW) {  // a closest query's ray travels in the query record
+          stu(F_LIGHT, (uint32_t)light);
+          stu(F_LS, (uint32_t)ls);
+          stf(F_VIS, vis);
+          stf(F_FIN, fin.x); stf(F_FIN + 1, fin.y); stf(F_FIN + 2, fin.z);
+          if (st0 != ST_SHADOW) {  // shadow -> shadow steps never change the ray or the hit
+            stf(F_RAY, ray.o.x); stf(F_RAY + 1, ray.o.y); stf(F_RAY + 2, ray.o.z);
+            stf(F_RAY + 3, ray.d.x); stf(F_RAY + 4, ray.d.y); stf(F_RAY + 5, ray.d.z);
+            stf(F_RAY + 6, ray.time);
+            stf(F_HP, hp.x); stf(F_HP + 1, hp.y); stf(F_HP + 2, hp.z);
+            stf(F_HN, hn.x); stf(F_HN + 1, hn.y); stf(F_HN + 2, hn.z);
+            stu(F_MAT, (uint32_t)mat_id);
+            if (kTex) {
+              stf(F_UV, hu);
+              stf(F_UV + 1, hv);
+            }
+          }
+        }
         float* Q = a.query;
         Q[(Q_O + 0) * N + slot] = qo.x; Q[(Q_O + 1) * N + slot] = qo.y; Q[(Q_O + 2) * N + slot] = qo.z;
         Q[(Q_D + 0) * N + slot] = qd.x; Q[(Q_D + 1) * N + slot] = qd.y; Q[(Q_D + 2) * N + slot] = qd.z;
