@@ -55,25 +55,33 @@ def parse():
     ap.add_argument("--scene", default=None, help="render this scene.json instead of the soup")
     ap.add_argument("--cpu-rows", type=int, default=12, help="rows of the frame in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-traffic", default=None, help="JSON with per-launch HBM bytes from rocprofv3 --pmc")
+    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
+                    help="concurrent reference processes for the all-cores CPU figure (<= 1: skip)")
+    ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+                    help="JSON with per-launch HBM bytes of trace_kernel from rocprofv3 --pmc (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def cpu_baseline(scene_path: str, args, rank: int):
-    """Reference CPU path on a bounded sample: a centred band of rows of the same frame."""
+def _cpu_cmd(scene_path: str, args, y0: int, y1: int):
+    W = args.res
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    if os.path.exists(ref):
+        return [ref, "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt), "-light_sample", "1",
+                "-seed", "42", "-rows", str(y0), str(y1)], "reference"
+    return [os.path.join(ROOT, "oracle", "oracle_cli"), "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt),
+            "-light_sample", "1", "-rng", "counter", "-seed", str(args.seed), "-region", "0", str(y0), str(W),
+            str(y1 - y0)], "port"
+
+
+def cpu_baseline(scene_path: str, args, rank: int):
+    """Reference CPU path on a bounded sample: a centred band of rows of the same frame, on
+    one core; then the same band size on each of N cores at once, as N
+    concurrent single-threaded processes on disjoint bands (the reference cannot split one
+    image across threads)."""
     W = H = args.res
     y0 = H // 2 - args.cpu_rows // 2
     y1 = y0 + args.cpu_rows
-    if os.path.exists(ref):
-        cmd = [ref, "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt), "-light_sample", "1",
-               "-seed", "42", "-rows", str(y0), str(y1)]
-        kind = "reference"
-    else:
-        cmd = [os.path.join(ROOT, "oracle", "oracle_cli"), "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt),
-               "-light_sample", "1", "-rng", "counter", "-seed", str(args.seed), "-region", "0", str(y0), str(W),
-               str(y1 - y0)]
-        kind = "port"
+    cmd, kind = _cpu_cmd(scene_path, args, y0, y1)
     if not os.path.exists(cmd[0]):
         return None
     t0 = time.time()
@@ -85,12 +93,36 @@ def cpu_baseline(scene_path: str, args, rank: int):
     st = json.loads(r.stdout.strip().splitlines()[-1])
     rays = st["rays"]
     secs = st["render_seconds"]
-    return {
+    out = {
         "value": rays / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": kind,
         "sample": (f"rows {y0}-{y1 - 1} of the {W}x{H} frame at {args.spp_sqrt ** 2} spp "
                    f"({W * (y1 - y0)} px, {rays} rays, render {secs:.1f} s single-threaded; "
                    f"scene load + BVH build {st['load_seconds']:.1f} s excluded; wall {wall:.1f} s)"),
     }
+    n = args.cpu_procs
+    if n > 1:
+        # disjoint bands of the same height, packed around the centre of the frame
+        band = args.cpu_rows
+        first = max(0, H // 2 - (n * band) // 2)
+        jobs = []
+        for k in range(n):
+            a0 = min(H - band, first + k * band)
+            c, _ = _cpu_cmd(scene_path, args, a0, a0 + band)
+            jobs.append(subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd="/tmp"))
+        rates, total = [], 0
+        for j in jobs:
+            so, se = j.communicate()
+            if j.returncode != 0:
+                log("cpu baseline (all cores) failed:", se[-1000:])
+                return out
+            stk = json.loads(so.strip().splitlines()[-1])
+            rates.append(stk["rays"] / stk["render_seconds"] / 1e6)
+            total += stk["rays"]
+        out["value_all_cores"] = sum(rates)
+        out["cores_all"] = n
+        out["sample_all_cores"] = (f"{n} concurrent single-threaded processes, {band} rows each "
+                                   f"({total} rays); value = sum of the per-process render rates")
+    return out
 
 
 def main():
@@ -195,9 +227,14 @@ def main():
     avg_launch_ms = trace_ms_all / max(launches_all, 1)
     avg_launch_bytes = alg_bytes_all / max(launches_all, 1)
     achieved = avg_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
-    traffic = None
+    # HBM bytes per trace launch measured by rocprofv3 PMC passes of this same bench
+    # (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE); committed with the kernel version
+    # it was measured on (`label`)
+    traffic, traffic_src = None, None
     if args.pmc_traffic and os.path.exists(args.pmc_traffic):
-        traffic = json.load(open(args.pmc_traffic)).get("hbm_bytes_per_launch")
+        pm = json.load(open(args.pmc_traffic))
+        traffic = pm.get("hbm_bytes_per_launch")
+        traffic_src = f"{os.path.relpath(args.pmc_traffic, ROOT)} ({pm.get('label', '')})"
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(scene_path, args, rank)
@@ -223,6 +260,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_unit": "HBM bytes per trace launch", "traffic_source": traffic_src,
+            "alg_bytes_per_launch": int(avg_launch_bytes),
             "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
             "alg_bytes_per_ray": round(bytes_per_ray, 1), "launches_per_step": int(launches_all / args.steps),
             "trace_share_of_step": round(trace_ms_all / world / (elapsed * 1e3), 3),
