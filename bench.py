@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--scene", default=None, help="render this scene.json instead of the soup")
     ap.add_argument("--cpu-rows", type=int, default=12, help="rows of the frame in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--primary-only", action="store_true",
+                    help="SURVEY.md 8(d) C2 BVH-stress variant: the soup without lights (one ray per sample)")
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="concurrent reference processes for the all-cores CPU figure (<= 1: skip)")
     ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
@@ -147,10 +149,18 @@ def main():
         scene_path = args.scene
         workload = os.path.basename(args.scene)
     else:
-        scene_path = f"/tmp/rt_bench_soup_{args.tris}_{args.res}_{rank}.json"
+        tag = "_nolights" if args.primary_only else ""
+        scene_path = f"/tmp/rt_bench_soup_{args.tris}_{args.res}{tag}_{rank}.json"
         if not os.path.exists(scene_path):
             rt.make_soup(scene_path, args.tris, seed=20251226, width=args.res, height=args.res)
+            if args.primary_only:  # the soup with "lights": [] -> 1 ray/sample
+                txt = open(scene_path).read()
+                i = txt.index('"lights": [')
+                j = txt.index("\n", i)
+                open(scene_path, "w").write(txt[:i] + '"lights": [],' + txt[j:])
         workload = f"synthetic triangle soup, {args.tris} triangles (planes c3=c0), splitmix64 seed 20251226"
+        if args.primary_only:
+            workload += ", no lights (primary rays only)"
     t0 = time.time()
     scene = rt.Scene(scene_path, resolution=(args.res, args.res))
     load_s = time.time() - t0
