@@ -10,6 +10,11 @@
   floor rectangle, a textured quad plane and two triangles (planes with c3 == c0), a hard
   and a soft (radius > 0) light, optional thin-lens depth of field.
 * ``soup(...)``       -- a seeded triangle soup written as ``planes`` with c3 == c0.
+* ``blend(name, ...)`` -- the reference's own Blender scenes (/root/reference/Blend/*.blend),
+  exported by tools/blend_export.py (byte-identical to the reference exporter's output on
+  Test2.blend -> ASCII/scene.json) and committed under tests/golden/scenes/blend/: the
+  BASELINE configs C3 (Antialiasing) and C4 (glossy_reflection + soft shadows), and the DOF,
+  motion-blur, soft-shadow and sphere scenes, at small resolutions.
 Scenes are plain dicts; ``write(scene, path)`` dumps JSON whose floats round-trip exactly.
 """
 from __future__ import annotations
@@ -119,6 +124,16 @@ def soup(n=200, seed=5, res=(48, 48), light=True) -> dict:
 
 
 # name -> (scene builder, CLI-equivalent render args).  These are the golden-vector cases.
+def blend(name: str, res=(48, 32), light_radius=None) -> dict:
+    with open(os.path.join(GOLDEN, "scenes", "blend", name + ".json")) as f:
+        s = json.load(f)
+    s["render"] = {"resolution_x": res[0], "resolution_y": res[1]}
+    if light_radius is not None:  # soft shadows via light radius > 0
+        for light in s["lights"]:
+            light["radius"] = light_radius
+    return s
+
+
 def cases() -> dict:
     return {
         "ascii_k1_bvh": (lambda: ascii((64, 64), roughness=0.0), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
@@ -133,6 +148,14 @@ def cases() -> dict:
         "soup_s1": (lambda: soup(300, seed=11), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
         "soup_s3": (lambda: soup(120, seed=3, res=(32, 32)), dict(use_bvh=True, spp_sqrt=3, light_samples=1)),
         "soup_linear": (lambda: soup(80, seed=4, res=(32, 32)), dict(use_bvh=False, spp_sqrt=1, light_samples=1)),
+        "blend_c3_antialiasing": (lambda: blend("Antialiasing", (64, 48)), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
+        "blend_c4_glossy_soft": (lambda: blend("glossy_reflection", (64, 48), light_radius=1.0),
+                                 dict(use_bvh=True, spp_sqrt=2, light_samples=2)),
+        "blend_dop": (lambda: blend("dop"), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
+        "blend_motion_blur": (lambda: blend("motion_blur"), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
+        "blend_distributed": (lambda: blend("Distributed"), dict(use_bvh=True, spp_sqrt=1, light_samples=2)),
+        "blend_test1": (lambda: blend("Test1"), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
+        "blend_test3": (lambda: blend("Test3"), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
     }
 
 

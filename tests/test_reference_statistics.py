@@ -22,9 +22,10 @@ import scenes
 
 SEED = 20251226
 STAT_TOL = 0.03
-DETERMINISTIC = ["ascii_k1_bvh", "ascii_primary", "soup_linear", "soup_s1"]
+DETERMINISTIC = ["ascii_k1_bvh", "ascii_primary", "soup_linear", "soup_s1", "blend_test3"]
 STOCHASTIC = ["ascii_glossy_bvh", "ascii_glossy_s2_linear", "ascii_textured", "features_dof", "features_linear",
-              "features_s1", "features_s2_ls3", "soup_s3"]
+              "features_s1", "features_s2_ls3", "soup_s3", "blend_c3_antialiasing", "blend_c4_glossy_soft",
+              "blend_distributed", "blend_dop", "blend_motion_blur", "blend_test1"]
 
 MAN = json.load(open(os.path.join(scenes.GOLDEN, "manifest.json")))
 
