@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--scene", default=None, help="render this scene.json instead of the soup")
     ap.add_argument("--cpu-rows", type=int, default=12, help="rows of the frame in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--light-samples", type=int, default=1, help="-light_sample (shadow rays per light with radius > 0)")
+    ap.add_argument("--light-radius", type=float, default=None,
+                    help="override every light's radius (SURVEY.md 8(d) C4: soft shadows, e.g. 1.0)")
     ap.add_argument("--primary-only", action="store_true",
                     help="SURVEY.md 8(d) C2 BVH-stress variant: the soup without lights (one ray per sample)")
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
@@ -68,10 +71,11 @@ def _cpu_cmd(scene_path: str, args, y0: int, y1: int):
     W = args.res
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
     if os.path.exists(ref):
-        return [ref, "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt), "-light_sample", "1",
+        return [ref, "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt), "-light_sample", str(args.light_samples),
                 "-seed", "42", "-rows", str(y0), str(y1)], "reference"
     return [os.path.join(ROOT, "oracle", "oracle_cli"), "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt),
-            "-light_sample", "1", "-rng", "counter", "-seed", str(args.seed), "-region", "0", str(y0), str(W),
+            "-light_sample", str(args.light_samples), "-rng", "counter", "-seed", str(args.seed), "-region", "0",
+            str(y0), str(W),
             str(y1 - y0)], "port"
 
 
@@ -148,6 +152,16 @@ def main():
     if args.scene:
         scene_path = args.scene
         workload = os.path.basename(args.scene)
+        # the same file for the GPU and the CPU baseline: resolution (and light radius) set here
+        sc_json = json.load(open(args.scene))
+        sc_json["render"] = {"resolution_x": args.res, "resolution_y": args.res}
+        if args.light_radius is not None:
+            for light in sc_json.get("lights", []):
+                light["radius"] = args.light_radius
+            workload += f", light radius {args.light_radius}"
+        scene_path = f"/tmp/rt_bench_scene_{os.getpid()}_{rank}.json"
+        with open(scene_path, "w") as f:
+            json.dump(sc_json, f)
     else:
         tag = "_nolights" if args.primary_only else ""
         scene_path = f"/tmp/rt_bench_soup_{args.tris}_{args.res}{tag}_{rank}.json"
@@ -175,7 +189,7 @@ def main():
     log(f"[rank {rank}] scene {W}x{H}, {scene.info.n_shapes} shapes, {scene.info.n_nodes} nodes, depth "
         f"{scene.info.tree_depth}, load+build {load_s:.1f} s; {len(mine)} tiles on cuda:{dev}")
 
-    params = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=1, use_bvh=True, seed=args.seed)
+    params = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=args.seed)
 
     def step(seed):
         nonlocal gathered
@@ -186,7 +200,8 @@ def main():
         return st
 
     # ---- instrumented frame: algorithmic bytes per ray (same seed as the first timed step)
-    cp = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=1, use_bvh=True, seed=args.seed, count_work=True)
+    cp = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=args.seed,
+                         count_work=True)
     cst = ds.render_tiles(mine, T, T, out.data_ptr(), cp)
     bytes_per_ray = (NODE_BYTES * cst.box_tests + PRIM_BYTES * cst.prim_tests) / max(cst.rays, 1)
     log(f"[rank {rank}] instrumented: rays {cst.rays}, box tests {cst.box_tests} ({cst.box_tests / max(cst.rays, 1):.1f}/ray),"
@@ -263,7 +278,7 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": workload,
-            "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample 1",
+            "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample {args.light_samples}",
             "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}",
             "rng": "counter (splitmix64 per pixel/sample)",
         },
