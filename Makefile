@@ -16,7 +16,7 @@ BIN := ray_tracying_amd/bin
 SRC := ray_tracying_amd/csrc
 COMMON_H := $(SRC)/common/rt_powf.h $(SRC)/common/glibc_powf_data.h include/rt_hip.h
 
-all: $(LIB)/librt_hip.so $(LIB)/librt_host.so $(BIN)/raytracer oracle
+all: $(LIB)/librt_hip.so $(LIB)/librt_host.so $(LIB)/librt_comm.so $(BIN)/raytracer oracle
 
 $(LIB)/librt_hip.so: $(SRC)/hip/rt_hip.hip $(SRC)/hip/rt_device.h $(COMMON_H)
 	@mkdir -p $(LIB)
@@ -26,9 +26,14 @@ HOST_SRC := $(SRC)/host/json_dom.cpp $(SRC)/host/scene.cpp $(SRC)/host/bvh_wide.
 $(LIB)/librt_host.so: $(HOST_SRC) $(SRC)/host/json_dom.hpp $(SRC)/host/scene.hpp include/rt_host.h $(COMMON_H) $(LIB)/librt_hip.so
 	$(CXX) $(CXXFLAGS) -shared $(HOST_SRC) -o $@ -L$(LIB) -lrt_hip -Wl,-rpath,'$$ORIGIN'
 
-$(BIN)/raytracer: $(SRC)/host/main.cpp $(LIB)/librt_host.so
+# RCCL collectives (librccl from ROCm) for the multi-GPU tile gather
+$(LIB)/librt_comm.so: $(SRC)/comm/rt_comm.cpp include/rt_comm.h include/rt_hip.h
+	@mkdir -p $(LIB)
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared $(SRC)/comm/rt_comm.cpp -o $@ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+$(BIN)/raytracer: $(SRC)/host/main.cpp $(LIB)/librt_host.so $(LIB)/librt_comm.so include/rt_comm.h
 	@mkdir -p $(BIN)
-	$(CXX) $(CXXFLAGS) $(SRC)/host/main.cpp -o $@ -L$(LIB) -lrt_host -lrt_hip -lpthread -Wl,-rpath,'$$ORIGIN/../lib'
+	$(CXX) $(CXXFLAGS) $(SRC)/host/main.cpp -o $@ -L$(LIB) -lrt_host -lrt_comm -lrt_hip -lpthread -Wl,-rpath,'$$ORIGIN/../lib'
 
 oracle:
 	$(MAKE) -C oracle all

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../../include/rt_hip.h"
+#include "../../../include/rt_comm.h"
 #include "../../../include/rt_host.h"
 
 int main(int argc, char* argv[]) {
@@ -95,43 +96,76 @@ int main(int argc, char* argv[]) {
     }
     rays = st.rays;
   } else {
-    // image-tile data parallelism: tile t goes to device (t mod gpus), one host thread each
+    // image-tile data parallelism: tile t goes to device (t mod gpus), one host thread per
+    // device renders into a packed device buffer (padded to the largest tile list), then one
+    // RCCL gather over xGMI brings every buffer to the first device (include/rt_comm.h)
     rt_scene_desc desc{};
     rt_camera_desc cam{};
     rth_scene_desc(scene, &desc);
     rth_scene_camera(scene, &cam);
     const int T = 64, tx = (width + T - 1) / T, ty = (height + T - 1) / T;
+    std::vector<std::vector<int32_t>> tiles(gpus);
+    for (int t = 0; t < tx * ty; ++t) tiles[t % gpus].push_back(t);
+    size_t max_tiles = 0;
+    for (auto& tl : tiles) max_tiles = std::max(max_tiles, tl.size());
+    const size_t count = max_tiles * T * T * 3;  // floats per rank
     std::vector<int> err(gpus, 0);
     std::vector<uint64_t> nr(gpus, 0);
+    std::vector<void*> d_out(gpus, nullptr);
+    std::vector<std::string> msg(gpus);
     std::vector<std::thread> th;
     for (int g = 0; g < gpus; ++g) {
       th.emplace_back([&, g]() {
-        std::vector<int32_t> tiles;
-        for (int t = g; t < tx * ty; t += gpus) tiles.push_back(t);
         rt_scene_t ds = nullptr;
-        if ((err[g] = rt_scene_create(device + g, &desc, &ds)) != 0) return;
-        size_t nv = tiles.size() * T * T * 3;
-        void* d_out = nullptr;
-        if ((err[g] = rt_malloc(device + g, nv * sizeof(float), &d_out)) != 0) { rt_scene_destroy(ds); return; }
+        if ((err[g] = rt_scene_create(device + g, &desc, &ds)) != 0) { msg[g] = rt_last_error(); return; }
+        if ((err[g] = rt_malloc(device + g, std::max<size_t>(count, 1) * sizeof(float), &d_out[g])) != 0) {
+          msg[g] = rt_last_error();
+          rt_scene_destroy(ds);
+          return;
+        }
         rt_stats st{};
-        err[g] = rt_render_tiles(ds, &cam, &p, tiles.data(), (int32_t)tiles.size(), T, T, (float*)d_out, nullptr, &st);
-        std::vector<float> packed(nv);
-        if (!err[g]) err[g] = rt_memcpy_d2h(packed.data(), d_out, nv * sizeof(float));
-        if (!err[g]) rth_unpack_tiles(packed.data(), tiles.data(), (int32_t)tiles.size(), T, T, width, height, rgb.data());
+        if (!tiles[g].empty())
+          err[g] = rt_render_tiles(ds, &cam, &p, tiles[g].data(), (int32_t)tiles[g].size(), T, T, (float*)d_out[g],
+                                   nullptr, &st);
+        if (err[g]) msg[g] = rt_last_error();
         nr[g] = st.rays;
-        rt_free(d_out);
         rt_scene_destroy(ds);
       });
     }
     for (auto& t : th) t.join();
-    for (int g = 0; g < gpus; ++g) {
-      if (err[g]) {
-        std::cerr << "An error occurred: device " << device + g << ": " << rt_last_error() << std::endl;
-        rth_scene_free(scene);
-        return 1;
+    int bad = -1;
+    for (int g = 0; g < gpus; ++g)
+      if (err[g]) bad = g;
+    std::vector<int32_t> devs(gpus);
+    for (int g = 0; g < gpus; ++g) devs[g] = device + g;
+    void* d_all = nullptr;
+    rt_comm_t comm = nullptr;
+    std::string cerr_msg;
+    if (bad < 0) {
+      std::vector<const float*> sends(gpus);
+      for (int g = 0; g < gpus; ++g) sends[g] = (const float*)d_out[g];
+      if (rt_malloc(device, (size_t)gpus * count * sizeof(float), &d_all) != 0 || rt_comm_create(gpus, devs.data(), &comm) != 0 ||
+          rt_comm_gather_f32(comm, sends.data(), count, (float*)d_all, 0) != 0) {
+        cerr_msg = std::string(rt_comm_last_error()) + " " + rt_last_error();
+      } else {
+        std::vector<float> packed((size_t)gpus * count);
+        if (rt_memcpy_d2h(packed.data(), d_all, packed.size() * sizeof(float)) != 0) cerr_msg = rt_last_error();
+        for (int g = 0; g < gpus && cerr_msg.empty(); ++g)
+          rth_unpack_tiles(packed.data() + (size_t)g * count, tiles[g].data(), (int32_t)tiles[g].size(), T, T, width,
+                           height, rgb.data());
       }
-      rays += nr[g];
     }
+    if (comm) rt_comm_destroy(comm);
+    if (d_all) rt_free(d_all);
+    for (void* d : d_out)
+      if (d) rt_free(d);
+    if (bad >= 0 || !cerr_msg.empty()) {
+      std::cerr << "An error occurred: "
+                << (bad >= 0 ? "device " + std::to_string(device + bad) + ": " + msg[bad] : cerr_msg) << std::endl;
+      rth_scene_free(scene);
+      return 1;
+    }
+    for (int g = 0; g < gpus; ++g) rays += nr[g];
   }
   double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   for (int y = 100; y < height; y += 100) std::cout << "Progress: " << (100 * y / height) << "%\n";

@@ -21,7 +21,8 @@ def declared(header):
     return set(re.findall(r"^\s*(?:const\s+)?[a-z_]+\**\s+\**(rth?_[a-z0-9_]+)\s*\(", txt, flags=re.M))
 
 
-@pytest.mark.parametrize("lib,header", [("librt_hip.so", "rt_hip.h"), ("librt_host.so", "rt_host.h")])
+@pytest.mark.parametrize("lib,header", [("librt_hip.so", "rt_hip.h"), ("librt_host.so", "rt_host.h"),
+                                        ("librt_comm.so", "rt_comm.h")])
 def test_c_abi_exports_every_declared_symbol(lib, header):
     path = os.path.join(rt.LIB_DIR, lib)
     syms = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
