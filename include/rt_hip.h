@@ -203,6 +203,12 @@ int rt_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
 int rt_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes);
 int rt_synchronize(int32_t device);
 
+/* Device-side pixel finalisation (raytracer.cpp:446-457 + Image::setPixel, image.cpp:28-37):
+ * out[i] = clamp((int)(clamp(powf(rgb[i], 1.0f/1.1f), 0, 1) * 255.999), 0, 255), with the
+ * bit-exact glibc powf restatement -- equal to rth_quantise byte for byte.  d_rgb / d_u8 are
+ * device pointers on the current device; stream may be NULL; returns after enqueueing. */
+int rt_quantise_device(const float* d_rgb, int64_t n, uint8_t* d_u8, void* stream);
+
 /* Identification of the compiled device code (e.g. "gfx950"). */
 const char* rt_build_info(void);
 const char* rt_last_error(void);

@@ -98,6 +98,7 @@ _host = None
 HIP_SYMBOLS = [
     "rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_tiles", "rt_malloc",
     "rt_free", "rt_memcpy_d2h", "rt_memcpy_h2d", "rt_synchronize", "rt_build_info", "rt_last_error",
+    "rt_quantise_device",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_free", "rth_scene_get_info", "rth_scene_desc", "rth_scene_camera",
@@ -135,6 +136,7 @@ def _load():
     _hip.rt_free.argtypes = [c.c_void_p]
     _hip.rt_memcpy_d2h.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     _hip.rt_memcpy_h2d.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
+    _hip.rt_quantise_device.argtypes = [c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p]
     _hip.rt_synchronize.argtypes = [c.c_int32]
     _host.rth_last_error.restype = c.c_char_p
     _host.rth_scene_load.argtypes = [c.c_char_p, c.c_char_p, c.c_int32, c.c_int32, c.POINTER(c.c_void_p)]
@@ -321,6 +323,13 @@ def quantise(rgb: np.ndarray) -> np.ndarray:
     out = np.empty(a.shape, dtype=np.uint8)
     _check_host(_host.rth_quantise(a.ctypes.data, int(a.size), out.ctypes.data), "rth_quantise")
     return out
+
+
+def quantise_device(d_rgb: int, n: int, d_u8: int, stream: int = 0):
+    """Device-side quantise (rt_quantise_device): n floats at device pointer d_rgb -> n bytes
+    at d_u8, byte-identical to quantise(); enqueued on `stream` (0 = default)."""
+    _load()
+    _check_hip(_hip.rt_quantise_device(d_rgb, int(n), d_u8, stream or None), "rt_quantise_device")
 
 
 def write_ppm(path: str, u8: np.ndarray):

@@ -817,6 +817,17 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
   a.out[off + 2] = c.z;
 }
 
+// pixel finalisation (raytracer.cpp:446-457, image.cpp:28-37), the same ops as rth_quantise
+__global__ __launch_bounds__(kBlock) void quantise_kernel(const float* rgb, long long n, uint8_t* out) {
+  const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float gamma = 1.1f;
+  const float g = rt_powf(rgb[i], 1.0f / gamma);
+  const float c = smax(0.0f, smin(1.0f, g));
+  const int v = static_cast<int>((double)c * 255.999);
+  out[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
 // slot initialisation: slot k takes unit k (units past the end retire immediately); a unit
 // whose pixel is outside the image (edge tiles) is skipped by the first logic step.
 __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, long long n_units, int* result,
@@ -1202,6 +1213,15 @@ int rt_memcpy_h2d(void* d, const void* h, size_t bytes) {
 int rt_synchronize(int32_t device) {
   HIP_TRY(hipSetDevice(device), RT_EDEVICE);
   HIP_TRY(hipDeviceSynchronize(), RT_EDEVICE);
+  return RT_OK;
+}
+
+int rt_quantise_device(const float* d_rgb, int64_t n, uint8_t* d_u8, void* stream) {
+  if (n < 0 || (n > 0 && (!d_rgb || !d_u8))) return fail(RT_EINVAL, "rt_quantise_device: bad argument");
+  if (n == 0) return RT_OK;
+  const unsigned blocks = (unsigned)((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(quantise_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, d_rgb, (long long)n, d_u8);
+  HIP_TRY(hipGetLastError(), RT_EDEVICE);
   return RT_OK;
 }
 

@@ -91,3 +91,19 @@ def test_tile_order_and_subset_independence(tmp_path, gpu):
     assert np.array_equal(img2.view(np.uint32), full.view(np.uint32))
     ds.close()
     sc.close()
+
+
+def test_device_quantise_matches_host(gpu):
+    """rt_quantise_device (device pixel finalisation) == rth_quantise
+    byte for byte, over every float class the framebuffer can hold and a dense sweep."""
+    import torch
+    rng = np.random.default_rng(7)
+    special = np.array([0.0, -0.0, 1.0, 0.5, 1e-30, 1e-45, -1e-3, 2.0, 1e30, np.inf, -np.inf, np.nan,
+                        np.float32(1.0) - np.float32(2 ** -24), 0.1, 0.099999994], dtype=np.float32)
+    vals = np.concatenate([special, rng.random(200000, dtype=np.float32) * 1.2 - 0.1,
+                           np.linspace(0, 1, 100001, dtype=np.float32)])
+    d = torch.from_numpy(vals).to("cuda")
+    out = torch.empty(vals.size, dtype=torch.uint8, device="cuda")
+    rt.quantise_device(d.data_ptr(), vals.size, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), rt.quantise(vals))
