@@ -87,7 +87,9 @@ typedef struct rt_node4 {
 
 /* Per primitive (in traversal order): its position in the reference's BVH-sorted list
  * (the tie-break order for equal t, acceleration.cpp:112/133) and the reference leaf that
- * holds it (index into ref_leaf_boxes). */
+ * holds it (index into ref_leaf_boxes), or -1 when the host proved that the reference leaf
+ * test passes for every hit the primitive can report (bvh_wide.cpp: acceptance region inside
+ * the leaf box shrunk by 1e-5 * scale), so the kernel skips it. */
 typedef struct rt_prim_ref {
   int32_t ref_index;
   int32_t ref_leaf;

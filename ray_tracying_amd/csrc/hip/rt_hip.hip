@@ -43,7 +43,14 @@ namespace {
 
 constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
 constexpr int kBlock = 256;
-constexpr int kLdsStack = 16;
+constexpr int kLdsStack = 16;  // default LDS stack entries per lane (RT_LDS_STACK overrides)
+static int lds_stack_entries() {
+  static const int v = [] {
+    const char* e = std::getenv("RT_LDS_STACK");
+    return e ? std::max(1, std::min(64, std::atoi(e))) : kLdsStack;
+  }();
+  return v;
+}
 constexpr int kBatchShards = 32;  // sharded work counters: no hot atomic word  // traversal stack entries per lane held in LDS (rest spill to HBM)
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
@@ -145,6 +152,29 @@ __device__ __forceinline__ bool ref_leaf_ok(const TraceArgs& a, int leaf, const 
   return aabb_exact(blo, bhi, r, par, tn);
 }
 
+// Plane hit at parameter t.  The primitive's reference leaf box contains the plane's own box,
+// corners -/+ 1e-4f (Plane::get_bounding_box, shapes.cpp:496-503).  A hit point inside that
+// box by 2 * eps_abs (eps_abs = 1e-5 * scale) passes the reference's exact slab test on the
+// leaf box: along an axis with |d| >= 1e-6 its computed slab bounds err by at most
+// |bound - o| * 2^-23 <= 2 * scale * 2^-23, along a near-parallel axis the origin lies within
+// |P - o| * 1e-6 <= 2e-6 * scale of the hit point (unit directions; P and o inside the scene
+// bound) -- both far below the margin.  Such hits skip ref_leaf_ok's six divisions and its
+// extra memory round trip; every other hit takes the exact test.
+__device__ __forceinline__ bool plane_leaf_fast_ok(const PrimA& P, const Ray& r, float t, float eps) {
+  const float m = 2.0f * eps;
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float c0 = P.a[k], c1 = P.a[4 + k], c2 = P.a[8 + k], c3 = P.a[12 + k];
+    const float lo = fminf(fminf(c0, c1), fminf(c2, c3)) - 1e-4f;
+    const float hi = fmaxf(fmaxf(c0, c1), fmaxf(c2, c3)) + 1e-4f;
+    const float p = o[k] + t * d[k];
+    ok = ok && (p - lo >= m) && (hi - p >= m);
+  }
+  return ok;
+}
+
 template <bool kCount, bool kPlanesOnly>
 __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cnt, const Ray& r, bool any, float tmax,
                                            uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
@@ -157,13 +187,18 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
     if (kCount) ++nprim;
     if (!prim_hit<false, kPlanesOnly>(P, rec, r, t, nullptr)) continue;
     const int2 ref = a.prim_refs[pi];
+    auto leaf_ok = [&]() {
+      if (!check_leaf || ref.y < 0) return true;
+      if ((kPlanesOnly || RT_TAG_KIND(prim_tag(P)) == RT_PRIM_PLANE) && plane_leaf_fast_ok(P, r, t, a.c.eps_abs))
+        return true;
+      return ref_leaf_ok(a, ref.y, r, par);
+    };
     if (any) {  // occluder iff t <= light_dist (raytracer.cpp:233)
-      if (!(t > tmax) && (!check_leaf || ref_leaf_ok(a, ref.y, r, par))) {
+      if (!(t > tmax) && leaf_ok()) {
         h.done = true;
         return;
       }
-    } else if ((t < h.best_t || (t == h.best_t && ref.x < h.best_ref)) &&
-               (!check_leaf || ref_leaf_ok(a, ref.y, r, par))) {
+    } else if ((t < h.best_t || (t == h.best_t && ref.x < h.best_ref)) && leaf_ok()) {
       h.best_t = t;
       h.best_ref = ref.x;
       h.best_idx = pi;
@@ -181,9 +216,9 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
   ca = c;
 }
 
-// 5 waves/SIMD (96 VGPRs, a few spills outside the node loop) measured 2% faster than 4
+// 4 waves/SIMD (<= 128 VGPRs, no spills); 5 waves needs 96 VGPRs and spills in the leaf path
 template <bool kCount, bool kPlanesOnly>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void trace_kernel(TraceArgs ta) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void trace_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_slots;
   const int lane = threadIdx.x & 63;
@@ -1004,7 +1039,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   {  // persistent trace grid: blocks resident per CU x CUs
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
-    const int lds_entries = std::min(d->stack_bound, kLdsStack);
+    const int lds_entries = std::min(d->stack_bound, lds_stack_entries());
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (d->prim_stride == 64 ? trace_kernel<false, true> : trace_kernel<false, false>), kBlock,
                                                      (size_t)lds_entries * kBlock * sizeof(int)) != hipSuccess || bpc < 1)
       bpc = 2;
@@ -1123,7 +1158,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.fetch = ctl + 1;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
-  ta.lds_entries = std::min(s->desc.stack_bound, kLdsStack);
+  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries());
   const unsigned trace_blocks = (unsigned)std::max(1, std::min(s->n_cu * s->trace_blocks_per_cu,
                                                                (n_slots + kBlock - 1) / kBlock));
   ta.n_threads = (int)trace_blocks * kBlock;
@@ -1147,6 +1182,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // ---- iterate logic -> trace until no slot issues a query
   double trace_ms = 0.0;
   int iters = 0;
+  int replay_iter = -1, replay_reps = 0;
+  if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
   for (;;) {
     HIP_TRY(hipMemsetAsync(ctl, 0, 8, stream), RT_EDEVICE);  // any_query + trace fetch counter
@@ -1166,6 +1203,30 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev_a, s->ev_b), RT_EDEVICE);
+    if (replay_iter == iters && replay_reps > 0 && !p->count_work) {
+      // diagnostic (RT_TRACE_REPLAY=iter:reps): re-trace this step's queries; the results
+      // are recomputed identically, so the frame is unchanged
+      float tot = 0.f, best = 1e30f;
+      unsigned long long rays0 = 0;
+      HIP_TRY(hipMemcpy(&rays0, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+      for (int k = 0; k < replay_reps; ++k) {
+        HIP_TRY(hipMemsetAsync(ctl + 1, 0, 4, stream), RT_EDEVICE);
+        HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
+        if (planes_only) hipLaunchKernelGGL((trace_kernel<false, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+        else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+        HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
+        HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
+        float m = 0.f;
+        HIP_TRY(hipEventElapsedTime(&m, s->ev_a, s->ev_b), RT_EDEVICE);
+        tot += m;
+        best = std::min(best, m);
+      }
+      unsigned long long rays1 = 0;
+      HIP_TRY(hipMemcpy(&rays1, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+      HIP_TRY(hipMemcpy(ctl + 8, &rays0, 8, hipMemcpyHostToDevice), RT_EDEVICE);  // keep the frame's ray count
+      std::fprintf(stderr, "[rt replay] step %d: %llu queries, trace %.4f ms avg / %.4f ms min over %d reps\n", iters,
+                   (rays1 - rays0) / (unsigned long long)replay_reps, tot / replay_reps, best, replay_reps);
+    }
     const bool more = *s->h_flag != 0;
     if (more) {  // the final (empty) trace launch is not a traversal step
       trace_ms += ms;

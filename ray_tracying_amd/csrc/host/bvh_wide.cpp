@@ -262,6 +262,8 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
   const int n = (int)sc.order.size();
   const float margin = 1e-5f * sc.scene_scale;
   std::vector<BuildPrim> bounded;
+  std::vector<Box> accept_box(n);          // unpadded acceptance region (planes)
+  std::vector<uint8_t> has_accept(n, 0);
   std::vector<int> unbounded;  // sorted positions
   std::vector<int> never;      // planes that accept no point: kept for indexing, never traversed
   bounded.reserve(n);
@@ -292,7 +294,11 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
       bool ne1 = false, ne2 = false;
       ok = tri_region(C[1], C[3], C[2], nn, 2e-6, region, ne1) && tri_region(C[0], C[1], C[2], nn, 2e-6, region, ne2);
       if (ok && !ne1 && !ne2) { never.push_back(r); continue; }  // accepts nothing
-      if (ok) b = region;
+      if (ok) {
+        b = region;
+        accept_box[r] = region;
+        has_accept[r] = 1;
+      }
     }
     for (int i = 0; i < 3; ++i) {
       b.lo[i] -= pad + std::fabs(b.lo[i]) * 2e-6f;
@@ -398,6 +404,23 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
     prims[i] = sc.prims[r];
     sc.prim_refs[i].ref_index = r;
     sc.prim_refs[i].ref_leaf = ref_leaf_of[r];
+    // The reference-leaf filter (AABB::intersect on the primitive's leaf box, shapes.cpp:55-72)
+    // is provably true for every hit this primitive can report when its acceptance region
+    // lies inside the leaf box shrunk by delta: along an axis with |d| >= 1e-6 the computed
+    // slab bounds are off by at most |bound - o| * 2^-23 <= 2 * scale * 2^-23 << delta, and
+    // along a near-parallel axis the origin is within |P - o| * 1e-6 <= 2e-6 * scale of the
+    // hit point (unit directions, |P - o| <= 2 * scale).  Such primitives carry ref_leaf = -1
+    // and the kernel skips the check (for c3 == c0 triangles the reference pads every plane
+    // box by 1e-4, so triangle soups qualify).
+    if (has_accept[r]) {
+      const double delta = 1e-5 * std::max(1.0, (double)sc.scene_scale);
+      const float* lb = &sc.ref_leaf_boxes[(size_t)ref_leaf_of[r] * 8];
+      bool inside = true;
+      for (int a = 0; a < 3; ++a)
+        inside = inside && (double)accept_box[r].lo[a] >= (double)lb[a] + delta &&
+                 (double)accept_box[r].hi[a] <= (double)lb[4 + a] - delta;
+      if (inside) sc.prim_refs[i].ref_leaf = -1;
+    }
   }
   sc.prims.swap(prims);
 }
