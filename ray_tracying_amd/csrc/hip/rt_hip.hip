@@ -225,6 +225,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
   unsigned int nrays = 0;
   const int gtid = blockIdx.x * kBlock + threadIdx.x;
   unsigned int nbox = 0, nprim = 0;
+  unsigned long long dg_any_rays = 0, dg_any_box = 0;  // kCount diagnostics: shadow (any-hit) queries
   const TraceArgs& a = ta;
   const int N = ta.n_slots;
   for (;;) {  // persistent: each wave pulls 64 queries at a time
@@ -238,6 +239,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     const int kind = __float_as_int(ta.query[Q_KIND * N + slot]);
     if (kind < 0) continue;  // no query from this slot in this step
     ++nrays;
+    if (kCount && (kind & 1)) ++dg_any_rays;
     Ray r;
     r.o = V3{ta.query[(Q_O + 0) * N + slot], ta.query[(Q_O + 1) * N + slot], ta.query[(Q_O + 2) * N + slot]};
     r.d = V3{ta.query[(Q_D + 0) * N + slot], ta.query[(Q_D + 1) * N + slot], ta.query[(Q_D + 2) * N + slot]};
@@ -300,6 +302,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         }
         if (kCount) nbox += __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
                                                 (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
+        if (kCount && any) dg_any_box += __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
+                                                              (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
         // leaves first (their hits tighten the bound before internal children are ordered);
         // one primitive-test instance walks the leaf bitmask (no 4x inlined copies)
         uint32_t leaves = 0;
@@ -370,6 +374,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
     if (lane == 0 && (b | p)) {
       atomicAdd(ta.counters + 0, b);
       atomicAdd(ta.counters + 1, p);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      dg_any_rays += __shfl_xor(dg_any_rays, off);
+      dg_any_box += __shfl_xor(dg_any_box, off);
+    }
+    if (lane == 0) {  // ctl byte 512
+      atomicAdd(ta.counters + 62, dg_any_rays);
+      atomicAdd(ta.counters + 63, dg_any_box);
     }
   }
 }
@@ -1183,6 +1195,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   double trace_ms = 0.0;
   int iters = 0;
   int replay_iter = -1, replay_reps = 0;
+  const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
+  unsigned long long diag_prev = 0;
   if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
   for (;;) {
@@ -1228,6 +1242,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
                    (rays1 - rays0) / (unsigned long long)replay_reps, tot / replay_reps, best, replay_reps);
     }
     const bool more = *s->h_flag != 0;
+    if (diag && more) {
+      unsigned long long rc = 0;
+      HIP_TRY(hipMemcpy(&rc, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+      std::fprintf(stderr, "[rt diag] step %2d: %9llu queries, trace %.3f ms (%.2f Gq/s)\n", iters, rc - diag_prev, ms,
+                   (double)(rc - diag_prev) / (ms * 1e6));
+      diag_prev = rc;
+    }
     if (more) {  // the final (empty) trace launch is not a traversal step
       trace_ms += ms;
       ++iters;
@@ -1249,6 +1270,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     stats->kernel_ms = ms;
     stats->trace_ms = trace_ms;
     stats->iterations = iters;
+    if (p->count_work && std::getenv("RT_DIAG")) {
+      unsigned long long dg[2] = {0, 0};
+      HIP_TRY(hipMemcpy(dg, ctl + 128, sizeof(dg), hipMemcpyDeviceToHost), RT_EDEVICE);
+      const unsigned long long cr = cnt[2] - dg[0], cb = cnt[0] - dg[1];
+      std::fprintf(stderr, "[rt diag] shadow rays %llu: %.1f box tests/ray; other rays %llu: %.1f box tests/ray\n", dg[0],
+                   (double)dg[1] / (double)std::max(dg[0], 1ull), cr, (double)cb / (double)std::max(cr, 1ull));
+    }
   }
   return RT_OK;
 }
