@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=12, help="rows of the frame in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--light-samples", type=int, default=1, help="-light_sample (shadow rays per light with radius > 0)")
+    ap.add_argument("--emulate", type=int, default=0,
+                    help="diagnostic: render only rank --emulate-rank's tiles of an N-way split on this one GPU")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--light-radius", type=float, default=None,
                     help="override every light's radius (SURVEY.md 8(d) C4: soft shadows, e.g. 1.0)")
     ap.add_argument("--primary-only", action="store_true",
@@ -183,8 +186,10 @@ def main():
     T = args.tile
     tiles_x, tiles_y = tl.tile_grid(W, H, T)
     n_tiles = tiles_x * tiles_y
-    mine = tl.assign_tiles(n_tiles, world, rank)
-    out = torch.zeros(tl.tiles_per_rank(n_tiles, world) * T * T * 3, dtype=torch.float32, device=f"cuda:{dev}")
+    mine = tl.assign_tiles(n_tiles, world, rank, tiles_x)
+    if args.emulate > 1 and world == 1:  # one rank's share of an N-way split (scaling prediction)
+        mine = tl.assign_tiles(n_tiles, args.emulate, args.emulate_rank, tiles_x)
+    out = torch.zeros(tl.tiles_per_rank(n_tiles, world, tiles_x) * T * T * 3, dtype=torch.float32, device=f"cuda:{dev}")
     gathered = None
     log(f"[rank {rank}] scene {W}x{H}, {scene.info.n_shapes} shapes, {scene.info.n_nodes} nodes, depth "
         f"{scene.info.tree_depth}, load+build {load_s:.1f} s; {len(mine)} tiles on cuda:{dev}")
@@ -281,6 +286,7 @@ def main():
             "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample {args.light_samples}",
             "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}",
             "rng": "counter (splitmix64 per pixel/sample)",
+            **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

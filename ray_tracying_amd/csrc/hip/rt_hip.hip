@@ -51,6 +51,9 @@ static int lds_stack_entries() {
   }();
   return v;
 }
+constexpr int kFetchShards = 8;    // trace work counters (one per XCD-sized slice of the slots)
+constexpr int kFetchStride = 32;   // u32 words between counters: one 128-B line each
+constexpr int kCtlBytes = 4096;    // control block; per-step reset region at byte 2048
 constexpr int kBatchShards = 32;  // sharded work counters: no hot atomic word  // traversal stack entries per lane held in LDS (rest spill to HBM)
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
@@ -124,7 +127,8 @@ struct TraceArgs {
   int n_nodes;
   const float* query;
   int* result;
-  unsigned int* fetch;        // persistent work counter over slots (zeroed per launch)
+  unsigned int* fetch;        // kFetchShards work counters over slot slices (zeroed per step)
+  const unsigned int* any_query;  // logic's "some slot has a query" flag for this step
   unsigned long long* rays;   // queries traced (one atomic per wave at exit)
   int n_slots;
   int lds_entries;            // traversal stack entries kept in LDS per lane
@@ -228,13 +232,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
   unsigned long long dg_any_rays = 0, dg_any_box = 0;  // kCount diagnostics: shadow (any-hit) queries
   const TraceArgs& a = ta;
   const int N = ta.n_slots;
-  for (;;) {  // persistent: each wave pulls 64 queries at a time
+  if (*ta.any_query == 0u) return;  // no slot emitted a query this step
+  // The slots are cut into kFetchShards slices with a counter each (one device-wide counter
+  // serialises at ~12 ns per 64-slot fetch: 1.6 ms per 8M-slot launch); a wave drains the
+  // slice of its block (blockIdx % 8 ~ its XCD) first, then helps the others.
+  const unsigned shard_len = (((nq + kFetchShards - 1) / kFetchShards) + 63u) & ~63u;
+  for (int sk = 0; sk < kFetchShards; ++sk) {
+   const int sh = (int)((blockIdx.x + sk) % kFetchShards);
+   const unsigned sh_start = (unsigned)sh * shard_len;
+   if (sh_start >= nq) continue;
+   const unsigned sh_len = min(shard_len, nq - sh_start);
+   unsigned int* ctr = ta.fetch + sh * kFetchStride;
+   for (;;) {  // persistent: each wave pulls 64 queries at a time
     unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(ta.fetch, 64u);
+    if (lane == 0) base = atomicAdd(ctr, 64u);
     base = __shfl(base, 0);
-    if (base >= nq) break;
-    const unsigned int qi = base + lane;
-    if (qi >= nq) continue;
+    if (base >= sh_len) break;
+    if (base + lane >= sh_len) continue;
+    const unsigned int qi = sh_start + base + lane;
     const int slot = (int)qi;
     const int kind = __float_as_int(ta.query[Q_KIND * N + slot]);
     if (kind < 0) continue;  // no query from this slot in this step
@@ -361,6 +376,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, any, tmax, par, true, h, nprim);
     }
     ta.result[slot] = any ? (h.done ? 1 : 0) : h.best_idx;
+   }
   }
   unsigned long long nr = nrays;
   for (int off = 32; off > 0; off >>= 1) nr += __shfl_xor(nr, off);
@@ -940,7 +956,7 @@ struct rt_scene_s {
   int* d_spill = nullptr;
   size_t spill_cap = 0;
   // per-render workspace (grown on demand)
-  void* d_ctl = nullptr;  // bytes 0: any_query (u32), 4: trace fetch (u32), 16/24: box/prim tests, 32: rays (u64),
+  void* d_ctl = nullptr;  // bytes 16/24: box/prim tests, 32: rays (u64), 2048: trace work counters, 3072: any_query,
                           // 256: batch counter shards (kBatchShards x u32)
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
@@ -1042,7 +1058,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     rt_scene_destroy(s);
     return rc;
   }
-  if (hipMalloc(&s->d_ctl, 1024) != hipSuccess || hipHostMalloc((void**)&s->h_flag, 64) != hipSuccess ||
+  if (hipMalloc(&s->d_ctl, kCtlBytes) != hipSuccess || hipHostMalloc((void**)&s->h_flag, 64) != hipSuccess ||
       hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
       hipEventCreate(&s->ev_a) != hipSuccess || hipEventCreate(&s->ev_b) != hipSuccess) {
     rt_scene_destroy(s);
@@ -1091,7 +1107,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const int n_samples = p->spp_sqrt <= 1 ? 1 : p->spp_sqrt * p->spp_sqrt;
   const long long n_units = (long long)n_pixels * n_samples;
   // whole blocks of slots; a wave renders 64 consecutive samples per batch
-  long long slot_cap = 1 << 23;  // 8M slots: ~16 fetches per trace wave per launch (measured best; 1M: -28%)
+  // Slots in flight: about a quarter of this call's samples, within [1M, 8M].  Whole frames
+  // (105M samples at 1024^2 x 100 spp) want 8M (1M: -28%: each persistent trace wave sees too
+  // few fetches and the launch tail dominates); one rank's share of an 8-way split (13M
+  // samples) wants ~3M (8M: +14% time from a long, sparse last step).
+  long long slot_cap = std::max(1LL << 20, std::min(1LL << 23, n_units / 4));
   if (const char* e = std::getenv("RT_SLOTS")) slot_cap = std::max(1LL << 12, std::atoll(e));
   const int n_slots = (int)(((std::min<long long>(n_units, slot_cap) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {
@@ -1120,7 +1140,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   }
   HIP_TRY(hipMemcpyAsync(s->d_tiles, tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream), RT_EDEVICE);
   unsigned int* ctl = (unsigned int*)s->d_ctl;
-  HIP_TRY(hipMemsetAsync(ctl, 0, 1024, stream), RT_EDEVICE);
+  HIP_TRY(hipMemsetAsync(ctl, 0, kCtlBytes, stream), RT_EDEVICE);
 
   LogicArgs la{};
   Common c{};
@@ -1156,7 +1176,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.refr = s->d_refr;
   la.query = s->d_query;
   la.result = s->d_result;
-  la.any_query = ctl;
+  la.any_query = ctl + 768;  // byte 3072
   la.batch_ctr = ctl + 64;  // byte 256
 
   TraceArgs ta{};
@@ -1167,7 +1187,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.n_nodes = s->desc.n_nodes;
   ta.query = s->d_query;
   ta.result = s->d_result;
-  ta.fetch = ctl + 1;
+  ta.fetch = ctl + 512;  // byte 2048: kFetchShards counters, 128 B apart
+  ta.any_query = ctl + 768;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries());
@@ -1200,10 +1221,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
   for (;;) {
-    HIP_TRY(hipMemsetAsync(ctl, 0, 8, stream), RT_EDEVICE);  // any_query + trace fetch counter
+    // per-step reset: trace work counters (byte 2048) + any_query (byte 3072)
+    HIP_TRY(hipMemsetAsync(ctl + 512, 0, kFetchShards * kFetchStride * 4 + 4, stream), RT_EDEVICE);
     launch_logic(la, need_frames, (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0, planes_only, slot_blocks, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipMemcpyAsync(s->h_flag, ctl, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipMemcpyAsync(s->h_flag, ctl + 768, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
     if (p->count_work) {
       if (planes_only) hipLaunchKernelGGL((trace_kernel<true, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
@@ -1224,7 +1246,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       unsigned long long rays0 = 0;
       HIP_TRY(hipMemcpy(&rays0, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
       for (int k = 0; k < replay_reps; ++k) {
-        HIP_TRY(hipMemsetAsync(ctl + 1, 0, 4, stream), RT_EDEVICE);
+        HIP_TRY(hipMemsetAsync(ctl + 512, 0, kFetchShards * kFetchStride * 4, stream), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
         if (planes_only) hipLaunchKernelGGL((trace_kernel<false, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
         else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);

@@ -105,7 +105,12 @@ int main(int argc, char* argv[]) {
     rth_scene_camera(scene, &cam);
     const int T = 64, tx = (width + T - 1) / T, ty = (height + T - 1) / T;
     std::vector<std::vector<int32_t>> tiles(gpus);
-    for (int t = 0; t < tx * ty; ++t) tiles[t % gpus].push_back(t);
+    // 2-D lattice deal, tile (x, y) -> (x + k*y) mod gpus with k >= gpus/2 coprime to gpus
+    // (ray_tracying_amd/tiles.py): every device samples the whole frame, not whole columns
+    int lk = std::max(1, (gpus + 1) / 2);
+    auto gcd = [](int a, int b) { while (b) { int t = a % b; a = b; b = t; } return a; };
+    while (gcd(lk, gpus) != 1) ++lk;
+    for (int t = 0; t < tx * ty; ++t) tiles[(t % tx + lk * (t / tx)) % gpus].push_back(t);
     size_t max_tiles = 0;
     for (auto& tl : tiles) max_tiles = std::max(max_tiles, tl.size());
     const size_t count = max_tiles * T * T * 3;  // floats per rank

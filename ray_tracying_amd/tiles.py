@@ -16,23 +16,49 @@ def tile_grid(width: int, height: int, tile: int) -> tuple[int, int]:
     return (width + tile - 1) // tile, (height + tile - 1) // tile
 
 
-def assign_tiles(n_tiles: int, world: int, rank: int) -> np.ndarray:
-    """Round-robin deal: tile t -> rank t % world."""
+def lattice_step(world: int) -> int:
+    """k for the deal (tx + k*ty) mod world: the smallest k >= world/2 coprime with world."""
+    k = max(1, (world + 1) // 2)
+    while np.gcd(k, world) != 1:
+        k += 1
+    return k
+
+
+def tile_rank(tid, tiles_x: int, world: int):
+    """2-D lattice deal: tile (tx, ty) -> rank (tx + k*ty) mod world.  Plain t mod world hands
+    every rank whole tile columns (the frame is usually a multiple of world tiles wide), so a
+    centred object loads a few ranks; the lattice spreads each rank over rows and columns
+    (a checkerboard for 2 ranks, spread diagonals for 4 and 8)."""
+    tid = np.asarray(tid)
+    return (tid % tiles_x + lattice_step(world) * (tid // tiles_x)) % world
+
+
+def assign_tiles(n_tiles: int, world: int, rank: int, tiles_x: int | None = None) -> np.ndarray:
+    """Tiles of `rank`, ascending.  tiles_x: tiles per image row (default: a square grid)."""
     ids = np.arange(n_tiles, dtype=np.int32)
-    return ids[ids % world == rank]
+    if world <= 1:
+        return ids
+    if tiles_x is None:
+        tiles_x = int(round(np.sqrt(n_tiles)))
+        if tiles_x * tiles_x != n_tiles:
+            raise ValueError("assign_tiles: pass tiles_x for a non-square tile grid")
+    return ids[tile_rank(ids, tiles_x, world) == rank]
 
 
-def tiles_per_rank(n_tiles: int, world: int) -> int:
-    return (n_tiles + world - 1) // world
+def tiles_per_rank(n_tiles: int, world: int, tiles_x: int | None = None) -> int:
+    """Largest per-rank tile count (the per-rank buffer size for the gather)."""
+    if world <= 1:
+        return n_tiles
+    return max(len(assign_tiles(n_tiles, world, r, tiles_x)) for r in range(world))
 
 
 def unpack(packed_per_rank, world: int, n_tiles: int, tile: int, width: int, height: int) -> np.ndarray:
-    """Assemble an image from each rank's packed tiles (rank r holds tiles r, r+world, ...)."""
+    """Assemble an image from each rank's packed tiles (rank r holds assign_tiles(..., r))."""
     img = np.zeros((height, width, 3), dtype=np.float32)
     tiles_x, _ = tile_grid(width, height, tile)
     for r in range(world):
         buf = np.asarray(packed_per_rank[r], dtype=np.float32).reshape(-1, tile, tile, 3)
-        for k, tid in enumerate(assign_tiles(n_tiles, world, r)):
+        for k, tid in enumerate(assign_tiles(n_tiles, world, r, tiles_x)):
             x0, y0 = (tid % tiles_x) * tile, (tid // tiles_x) * tile
             w, h = min(tile, width - x0), min(tile, height - y0)
             img[y0:y0 + h, x0:x0 + w] = buf[k, :h, :w]

@@ -23,8 +23,8 @@ def _worker(rank, world, port, scene_path, args, tile, q):
     W, H, _, _ = ob.scene_info(scene_path)
     tx, ty = tl.tile_grid(W, H, tile)
     n = tx * ty
-    mine = tl.assign_tiles(n, world, rank)
-    packed = np.zeros((tl.tiles_per_rank(n, world), tile, tile, 3), np.float32)
+    mine = tl.assign_tiles(n, world, rank, tx)
+    packed = np.zeros((tl.tiles_per_rank(n, world, tx), tile, tile, 3), np.float32)
     for k, tid in enumerate(mine):
         x0, y0 = (tid % tx) * tile, (tid // tx) * tile
         w, h = min(tile, W - x0), min(tile, H - y0)
@@ -63,9 +63,24 @@ def test_tiles_gather_equals_single_render(world, tmp_path):
 
 def test_assign_tiles_is_a_partition():
     from ray_tracying_amd import tiles as tl
-    for n in (1, 7, 256):
-        for world in (1, 2, 3, 8):
-            parts = [tl.assign_tiles(n, world, r) for r in range(world)]
+    for n, tx in ((1, 1), (7, 7), (12, 4), (256, 16), (1024, 32)):
+        for world in (1, 2, 3, 4, 6, 8):
+            parts = [tl.assign_tiles(n, world, r, tx) for r in range(world)]
             allt = np.sort(np.concatenate(parts))
             assert np.array_equal(allt, np.arange(n))
-            assert max(len(p) for p in parts) == tl.tiles_per_rank(n, world)
+            assert max(len(p) for p in parts) == tl.tiles_per_rank(n, world, tx)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_lattice_deal_balances_a_centred_object(world):
+    """The headline frame's work sits in the centre (the soup); plain t mod world would give
+    2 of 8 ranks the central columns.  With the lattice deal every rank's share of a centred
+    disc of tiles stays within 20% of the mean."""
+    from ray_tracying_amd import tiles as tl
+    tx = 16
+    yy, xx = np.mgrid[0:tx, 0:tx]
+    heavy = ((xx - 7.5) ** 2 + (yy - 7.5) ** 2 <= 5.5 ** 2).reshape(-1)
+    load = [heavy[tl.assign_tiles(tx * tx, world, r, tx)].sum() for r in range(world)]
+    assert max(load) <= 1.2 * np.mean(load), load
+    naive = [heavy[np.arange(tx * tx) % world == r].sum() for r in range(world)]
+    assert max(load) <= max(naive)

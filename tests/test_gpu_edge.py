@@ -83,8 +83,8 @@ def test_tile_order_and_subset_independence(tmp_path, gpu):
     from ray_tracying_amd import tiles as tl
     parts = []
     for r in range(2):
-        mine = tl.assign_tiles(n, 2, r)
-        b = torch.zeros(tl.tiles_per_rank(n, 2) * T * T * 3, dtype=torch.float32, device="cuda:0")
+        mine = tl.assign_tiles(n, 2, r, 4)
+        b = torch.zeros(tl.tiles_per_rank(n, 2, 4) * T * T * 3, dtype=torch.float32, device="cuda:0")
         ds.render_tiles(mine, T, T, b.data_ptr(), rt.RenderParams(spp_sqrt=2, light_samples=2, seed=77))
         parts.append(b.cpu().numpy())
     img2 = tl.unpack(parts, 2, n, T, 64, 48)
