@@ -71,8 +71,11 @@ enum Field : int {
   F_VIS,              // visibility accumulator of the current light
   F_FIN = F_VIS + 1,  // 3: shade's final_color
   F_UV = F_FIN + 3,   // 2: hit u, v (textures)
-  F_COUNT = F_UV + 2
+  F_KEY = F_UV + 2,   // 2: the sample's RNG stream key (lo, hi), set when the sample starts
+  F_COUNT = F_KEY + 2
 };
+// closest-hit record written by the trace kernel, one per slot: point, normal, u, v, material
+enum HitField : int { HIT_P = 0, HIT_N = 3, HIT_U = 6, HIT_V = 7, HIT_MAT = 8, HIT_COUNT = 9 };
 // query record, one per slot: o(3) d(3); TMAX = light distance (shadow) or ray time
 // (closest); KIND bit 0 = shadow any-hit
 enum QField : int { Q_O = 0, Q_D = 3, Q_TMAX = 6, Q_KIND = 7, Q_COUNT = 8 };
@@ -116,6 +119,7 @@ struct LogicArgs {
   float* refr;           // [kMaxDepth][6][n_slots] (null if no refraction)
   float* query;          // [Q_COUNT][n_slots]
   const int* result;     // [n_slots]
+  const float* hit;      // [HIT_COUNT][n_slots] (closest hits)
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
 };
 
@@ -135,6 +139,8 @@ struct TraceArgs {
   int* spill;                 // deeper entries: [entry - lds_entries][n_threads]
   int n_threads;              // threads of the persistent grid
   unsigned long long* counters;  // box tests, prim tests (count_work)
+  float* hit;                 // [HIT_COUNT][n_slots]: attributes of a closest hit (for the logic step)
+  int has_tex;                // some material is textured: hit u, v needed
 };
 
 // ---------------------------------------------------------------- traversal
@@ -376,6 +382,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, any, tmax, par, true, h, nprim);
     }
     ta.result[slot] = any ? (h.done ? 1 : 0) : h.best_idx;
+    if (!any && h.best_idx >= 0) {
+      // the hit record the Trace/shade step needs (raytracer.cpp:293-303): the same
+      // primitive test with attributes, on the primitive this lane just tested (cached)
+      const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
+      PrimA P;
+      load_prim_a(rec, P);
+      HitAttr at;
+      float t;
+      if (ta.has_tex) prim_hit<true, kPlanesOnly, true>(P, rec, r, t, &at);
+      else prim_hit<true, kPlanesOnly, false>(P, rec, r, t, &at);
+      float* H = ta.hit;
+      H[(HIT_P + 0) * N + slot] = at.p.x; H[(HIT_P + 1) * N + slot] = at.p.y; H[(HIT_P + 2) * N + slot] = at.p.z;
+      H[(HIT_N + 0) * N + slot] = at.n.x; H[(HIT_N + 1) * N + slot] = at.n.y; H[(HIT_N + 2) * N + slot] = at.n.z;
+      if (ta.has_tex) {
+        H[HIT_U * N + slot] = at.u;
+        H[HIT_V * N + slot] = at.v;
+      }
+      H[HIT_MAT * N + slot] = __uint_as_float(RT_TAG_MATERIAL(prim_tag(P)));
+    }
    }
   }
   unsigned long long nr = nrays;
@@ -533,10 +558,16 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       }
       const int res = st0 >= ST_CLOSEST ? a.result[slot] : -1;
       int px = 0, py = 0, sample = 0;
-      bool inside = unit >= 0 && unit_coords(a, unit, px, py, sample);
+      // the pixel / sample coordinates (64-bit division, tile lookups) are only needed when a
+      // sample starts; later steps continue its RNG stream from the stored key and counter
       Rng rng;
-      rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
-      rng.ctr = ld(F_RNG);
+      rng.key = 0;
+      rng.ctr = 0;
+      bool fresh = false;  // a sample started in this step: its RNG key goes to the state
+      if (st0 >= ST_CLOSEST) {
+        rng.key = (uint64_t)ld(F_KEY) | ((uint64_t)ld(F_KEY + 1) << 32);
+        rng.ctr = ld(F_RNG);
+      }
       bool retired = false;
       bool idle = unit == -2;
       V3 qo{0, 0, 0}, qd{0, 0, 0};
@@ -559,7 +590,7 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
         if (batch * 64 >= a.n_units || unit >= a.n_units) {
           retired = true;
         } else {
-          inside = unit_coords(a, unit, px, py, sample);
+          const bool inside = unit_coords(a, unit, px, py, sample);
           st = ST_SAMPLE;
           if (!inside) idle = true;  // edge tile: pixel outside the image
         }
@@ -571,6 +602,7 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
         if (st == ST_SAMPLE) {
           // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)
           rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
+          fresh = true;
           float fx, fy;
           if (s <= 1) {
             fx = (float)px + 0.5f;
@@ -600,17 +632,15 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
             ret = V3{0.1f, 0.1f, 0.1f};
             returning = true;
           } else {
-            const float4* rec = a.c.prims + (size_t)res * a.c.prim_stride4;
-            PrimA P;
-            load_prim_a(rec, P);
-            HitAttr at;
-            float t;
-            prim_hit<true, kPlanes, kTex>(P, rec, ray, t, &at);  // bit-identical to the traversal's test
-            hp = at.p;
-            hn = at.n;
-            hu = at.u;
-            hv = at.v;
-            mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
+            // hit attributes computed by the trace kernel (prim_hit<true> on this primitive)
+            const float* H = a.hit;
+            hp = V3{H[(HIT_P + 0) * N + slot], H[(HIT_P + 1) * N + slot], H[(HIT_P + 2) * N + slot]};
+            hn = V3{H[(HIT_N + 0) * N + slot], H[(HIT_N + 1) * N + slot], H[(HIT_N + 2) * N + slot]};
+            if (kTex) {
+              hu = H[HIT_U * N + slot];
+              hv = H[HIT_V * N + slot];
+            }
+            mat_id = (int)__float_as_uint(H[HIT_MAT * N + slot]);
             const rt_material& m = a.mats[mat_id];
             V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
             fin = V3{base.x * m.k_ambient, base.y * m.k_ambient, base.z * m.k_ambient};
@@ -804,6 +834,10 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
         stu(F_UNIT, (uint32_t)unit);
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
         stu(F_RNG, rng.ctr);
+        if (fresh) {
+          stu(F_KEY, (uint32_t)rng.key);
+          stu(F_KEY + 1, (uint32_t)(rng.key >> 32));
+        }
         if (st == ST_SHADOW) {  // a closest query's ray travels in the query record
           stu(F_LIGHT, (uint32_t)light);
           stu(F_LS, (uint32_t)ls);
@@ -967,17 +1001,18 @@ struct rt_scene_s {
   float* d_samples = nullptr;
   size_t samples_cap = 0;
   int* d_result = nullptr;
+  float* d_hit = nullptr;
   size_t slots_cap = 0;
   unsigned int* h_flag = nullptr;  // pinned
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_a = nullptr, ev_b = nullptr;
 };
 
 static void free_workspace(rt_scene_s* s) {
-  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples};
+  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples, s->d_hit};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
-  s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr;
+  s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr; s->d_hit = nullptr;
   s->slots_cap = 0;
   s->samples_cap = 0;
 }
@@ -1127,6 +1162,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_state, N * F_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_hit, N * HIT_COUNT * 4), RT_ENOMEM);
     if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
     if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
     s->slots_cap = N;
@@ -1176,6 +1212,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.refr = s->d_refr;
   la.query = s->d_query;
   la.result = s->d_result;
+  la.hit = s->d_hit;
   la.any_query = ctl + 768;  // byte 3072
   la.batch_ctr = ctl + 64;  // byte 256
 
@@ -1187,6 +1224,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.n_nodes = s->desc.n_nodes;
   ta.query = s->d_query;
   ta.result = s->d_result;
+  ta.hit = s->d_hit;
+  ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   ta.fetch = ctl + 512;  // byte 2048: kFetchShards counters, 128 B apart
   ta.any_query = ctl + 768;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
