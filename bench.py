@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec (primary+secondary), 1024x1024 @100spp; % HBM roofline"
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate over 8 XCDs
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 NODE_BYTES, PRIM_BYTES = 32, 64  # BASELINE.md / SURVEY.md 8(d) algorithmic bytes
 
@@ -67,6 +68,8 @@ def parse():
                     help="concurrent reference processes for the all-cores CPU figure (<= 1: skip)")
     ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="JSON with per-launch HBM bytes of trace_kernel from rocprofv3 --pmc (tools/pmc_traffic.py)")
+    ap.add_argument("--dump-frame", default=None,
+                    help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")
     return ap.parse_args()
 
 
@@ -143,12 +146,19 @@ def main():
     import ray_tracying_amd as rt
     from ray_tracying_amd import tiles as tl
 
+    # RT_BENCH_BACKEND=gloo: rehearsal of the N-rank path with more ranks than GPUs (ranks
+    # share devices, collectives through host memory) -- functional checks only, not a metric
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
     dist = None
+    dev = local_rank if backend == "nccl" else local_rank % max(torch.cuda.device_count(), 1)
+    coll = f"cuda:{dev}" if backend == "nccl" else "cpu"
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = local_rank
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(dev)
 
     # ---- scene: every rank builds the identical scene locally (deterministic generator)
@@ -201,7 +211,7 @@ def main():
         params.seed = seed
         st = ds.render_tiles(mine, T, T, out.data_ptr(), params)
         if dist:  # framebuffer gather to rank 0 over RCCL / xGMI
-            gathered = tl.gather_to_root(dist, out, rank, world)
+            gathered = tl.gather_to_root(dist, out if coll != "cpu" else out.cpu(), rank, world)
         return st
 
     # ---- instrumented frame: algorithmic bytes per ray (same seed as the first timed step)
@@ -234,8 +244,8 @@ def main():
     elapsed = time.perf_counter() - t0
 
     tot = torch.tensor([float(rays), trace_ms, float(launches), bytes_per_ray * rays], dtype=torch.float64,
-                       device=f"cuda:{dev}")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+                       device=coll)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll)
     if dist:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -245,6 +255,12 @@ def main():
     if rank == 0 and dist:  # sanity: the gathered frame has every pixel, all finite
         img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H)
         assert np.isfinite(img).all()
+    if args.dump_frame:  # one more frame at the first timed seed, gathered, saved by rank 0
+        step(args.seed)
+        torch.cuda.synchronize()
+        if rank == 0:
+            parts = [g.cpu().numpy() for g in gathered] if dist else [out.cpu().numpy()]
+            np.save(args.dump_frame, tl.unpack(parts, world, n_tiles, T, W, H))
 
     if rank != 0:
         if dist:
@@ -296,6 +312,10 @@ def main():
             "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
             "alg_bytes_per_ray": round(bytes_per_ray, 1), "launches_per_step": int(launches_all / args.steps),
             "trace_share_of_step": round(trace_ms_all / world / (elapsed * 1e3), 3),
+            # the tree + primitives (~0.1 GB) stay on-die: algorithmic bytes are served by L2 /
+            # Infinity Cache, so frac (vs HBM) can pass 1; the on-die ceiling is the L2's
+            "l2_peak": L2_PEAK_GBS, "frac_of_l2": round(achieved / L2_PEAK_GBS, 4),
+            "hbm_rate": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
         },
         "cpu_baseline": cpu,
     }

@@ -1142,11 +1142,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const int n_samples = p->spp_sqrt <= 1 ? 1 : p->spp_sqrt * p->spp_sqrt;
   const long long n_units = (long long)n_pixels * n_samples;
   // whole blocks of slots; a wave renders 64 consecutive samples per batch
-  // Slots in flight: about a quarter of this call's samples, within [1M, 8M].  Whole frames
-  // (105M samples at 1024^2 x 100 spp) want 8M (1M: -28%: each persistent trace wave sees too
-  // few fetches and the launch tail dominates); one rank's share of an 8-way split (13M
-  // samples) wants ~3M (8M: +14% time from a long, sparse last step).
-  long long slot_cap = std::max(1LL << 20, std::min(1LL << 23, n_units / 4));
+  // Slots in flight, sized to this call's samples (measured, 1024^2 x 100 spp soup): the whole
+  // frame (105M samples) runs best with 16M, one rank's share of a 2-way split (52M) with 13M,
+  // of a 4- or 8-way split (26M / 13M) with 6.5M.  Too few slots and each persistent trace wave
+  // sees few fetches (launch tails dominate); too many and the logic step pays for idle slots.
+  long long slot_cap = n_units < (20LL << 20) ? n_units / 2 : n_units / 4;
+  slot_cap = std::max(1LL << 20, std::min(1LL << 24, slot_cap));
   if (const char* e = std::getenv("RT_SLOTS")) slot_cap = std::max(1LL << 12, std::atoll(e));
   const int n_slots = (int)(((std::min<long long>(n_units, slot_cap) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {
