@@ -1074,6 +1074,18 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
   if (d->n_materials <= 0 || !d->materials) return fail(RT_EINVAL, "rt_scene_create: need >= 1 material");
   if (d->n_lights < 0 || (d->n_lights > 0 && !d->lights)) return fail(RT_EINVAL, "rt_scene_create: bad lights");
+  // every node reference in range and pointing forward (the kernel follows them unchecked)
+  const int64_t n_bounded = (int64_t)d->n_prims - d->n_unbounded;
+  for (int32_t i = 0; i < d->n_nodes; ++i) {
+    const rt_node4& nd = d->nodes[i];
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t m = (nd.meta >> (8 * k)) & 0xffu;
+      const int64_t c = nd.child[k];
+      const bool ok = m == 0 || (m == 0x01u && c > i && c < d->n_nodes) ||
+                      ((m & 0x80u) && (m & 0x7fu) != 0 && c >= 0 && c + (m & 0x7fu) <= n_bounded);
+      if (!ok) return fail(RT_EINVAL, "rt_scene_create: node child out of range");
+    }
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
     return fail(RT_ENODEV, "rt_scene_create: no such HIP device");
