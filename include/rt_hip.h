@@ -160,7 +160,7 @@ typedef struct rt_camera_desc {
 /* Render parameters: the reference's CLI flags (raytracer.cpp:361-390) + RNG key. */
 typedef struct rt_render_params {
   int32_t spp_sqrt;      /* -s  (<=1: one ray through the pixel centre) */
-  int32_t light_samples; /* -light_sample */
+  int32_t light_samples; /* -light_sample (0..65535; scenes hold at most 65535 lights) */
   int32_t use_bvh;       /* -bvh (0: linear search over all primitives, acceleration.cpp:124) */
   int32_t count_work;    /* 1: instrumented kernel, fills box_tests / prim_tests */
   uint64_t seed;         /* counter-RNG seed */

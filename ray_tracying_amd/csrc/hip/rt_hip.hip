@@ -58,21 +58,20 @@ constexpr int kBatchShards = 32;  // sharded work counters: no hot atomic word  
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
+// A word is read or written only where it carries information: the logic
+// step is bound by these bytes.  The hit being shaded is NOT copied here -- the trace
+// kernel's hit record stays intact while the slot traces only shadow queries.
 enum Field : int {
   F_UNIT = 0,  // work unit = launch-local pixel * n_samples + sample; -1 = slot retired
   F_CTRL,      // st | depth << 4
-  F_LIGHT,     // light index in shade
-  F_LS,        // shadow sample index for that light
-  F_RNG,       // draws consumed in the current sample
-  F_RAY,       // 7: o, d, time of the Trace at `depth`
-  F_HP = F_RAY + 7,   // 3: hit point
-  F_HN = F_HP + 3,    // 3: hit normal
-  F_MAT = F_HN + 3,   // material of the hit
-  F_VIS,              // visibility accumulator of the current light
-  F_FIN = F_VIS + 1,  // 3: shade's final_color
-  F_UV = F_FIN + 3,   // 2: hit u, v (textures)
-  F_KEY = F_UV + 2,   // 2: the sample's RNG stream key (lo, hi), set when the sample starts
-  F_COUNT = F_KEY + 2
+  F_LIGHT,     // light index in shade | shadow sample index for that light << 16
+  F_VIS,       // visibility accumulator of the current light (kept only while sample index > 0)
+  F_FIN,       // 3: shade's final_color (kept only from light 1 on: at light 0 it is the ambient term)
+  F_RNG = F_FIN + 3,  // draws consumed in the current sample  } only when a step after the
+  F_KEY,              // 2: the sample's RNG stream key        } sample's start can draw
+  F_RAY = F_KEY + 2,  // 7: o, d, time of the Trace at `depth` (without frames: o only, and
+                      // nothing for a pinhole camera, whose primary rays start at its location)
+  F_COUNT = F_RAY + 7
 };
 // closest-hit record written by the trace kernel, one per slot: point, normal, u, v, material
 enum HitField : int { HIT_P = 0, HIT_N = 3, HIT_U = 6, HIT_V = 7, HIT_MAT = 8, HIT_COUNT = 9 };
@@ -120,6 +119,8 @@ struct LogicArgs {
   float* query;          // [Q_COUNT][n_slots]
   const int* result;     // [n_slots]
   const float* hit;      // [HIT_COUNT][n_slots] (closest hits)
+  int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
+  int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
 };
 
@@ -519,14 +520,26 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
     auto stu = [&](int f, uint32_t v) { S[f * N + slot] = v; };
     auto stf = [&](int f, float v) { S[f * N + slot] = __float_as_uint(v); };
 
+    // One round of independent loads: the control words, the trace result and the RNG
+    // stream position are read for every slot whatever its state (a retired or idle slot
+    // discards them), so no load waits on another's value before the state-specific round.
     long long unit = (long long)(int)ld(F_UNIT);  // >= 0 active, -2 idle (batch done), -1 retired
+    const uint32_t ctrl0 = ld(F_CTRL);
+    const int res_ld = a.result[slot];
+    uint32_t key_lo = 0, key_hi = 0, rng_ctr = 0;
+    if (a.late_draws) {
+      key_lo = ld(F_KEY);
+      key_hi = ld(F_KEY + 1);
+      rng_ctr = ld(F_RNG);
+    }
     if (unit != -1) {
       const int s = a.spp_sqrt;
-      uint32_t ctrl = ld(F_CTRL);
+      uint32_t ctrl = ctrl0;
       int st = (int)(ctrl & 15u), depth = (int)(ctrl >> 4);
       // Only what the entry state reads is loaded: a closest-hit result needs the ray that
-      // was traced (still in the query record); a shadow result needs the hit and the
-      // shade accumulators; a new sample needs nothing.
+      // was traced (still in the query record) and the hit record (loaded before the result
+      // is known: a miss ignores it); a shadow result needs the hit and the shade
+      // accumulators; a new sample needs nothing.
       const int st0 = unit >= 0 ? st : -1;
       int light = 0, ls = 0, mat_id = 0;
       Ray ray;
@@ -535,28 +548,42 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       ray.time = 0.0f;
       V3 hp{0.0f, 0.0f, 0.0f}, hn{0.0f, 0.0f, 0.0f}, fin{0.0f, 0.0f, 0.0f};
       float vis = 0.0f, hu = 0.0f, hv = 0.0f;
-      if (st0 == ST_SHADOW) {
-        light = (int)ld(F_LIGHT);
-        ls = (int)ld(F_LS);
-        ray.o = V3{ldf(F_RAY), ldf(F_RAY + 1), ldf(F_RAY + 2)};
-        ray.d = V3{ldf(F_RAY + 3), ldf(F_RAY + 4), ldf(F_RAY + 5)};
-        ray.time = ldf(F_RAY + 6);
-        hp = V3{ldf(F_HP), ldf(F_HP + 1), ldf(F_HP + 2)};
-        hn = V3{ldf(F_HN), ldf(F_HN + 1), ldf(F_HN + 2)};
-        mat_id = (int)ld(F_MAT);
-        vis = ldf(F_VIS);
-        fin = V3{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
+      const V3 cam_o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
+      if (st0 == ST_SHADOW || st0 == ST_CLOSEST) {
+        // the hit being shaded: the trace kernel's record (prim_hit<true> on the hit primitive)
+        const float* H = a.hit;
+        hp = V3{H[(HIT_P + 0) * N + slot], H[(HIT_P + 1) * N + slot], H[(HIT_P + 2) * N + slot]};
+        hn = V3{H[(HIT_N + 0) * N + slot], H[(HIT_N + 1) * N + slot], H[(HIT_N + 2) * N + slot]};
         if (kTex) {
-          hu = ldf(F_UV);
-          hv = ldf(F_UV + 1);
+          hu = H[HIT_U * N + slot];
+          hv = H[HIT_V * N + slot];
         }
+        mat_id = (int)__float_as_uint(H[HIT_MAT * N + slot]);
+      }
+      if (st0 == ST_SHADOW) {
+        const uint32_t lw = ld(F_LIGHT);
+        light = (int)(lw & 0xffffu);
+        ls = (int)(lw >> 16);
+        if (kFrames) {
+          ray.o = V3{ldf(F_RAY), ldf(F_RAY + 1), ldf(F_RAY + 2)};
+          ray.d = V3{ldf(F_RAY + 3), ldf(F_RAY + 4), ldf(F_RAY + 5)};
+          ray.time = ldf(F_RAY + 6);
+        } else {  // shading reads only the origin
+          ray.o = a.pinhole ? cam_o : V3{ldf(F_RAY), ldf(F_RAY + 1), ldf(F_RAY + 2)};
+        }
+        if (ls > 0) vis = ldf(F_VIS);
+        if (light > 0) fin = V3{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
       } else if (st0 == ST_CLOSEST) {
         const float* Q = a.query;
-        ray.o = V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]};
-        ray.d = V3{Q[(Q_D + 0) * N + slot], Q[(Q_D + 1) * N + slot], Q[(Q_D + 2) * N + slot]};
-        ray.time = Q[Q_TMAX * N + slot];  // closest queries carry the ray time there
+        if (kFrames) {
+          ray.o = V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]};
+          ray.d = V3{Q[(Q_D + 0) * N + slot], Q[(Q_D + 1) * N + slot], Q[(Q_D + 2) * N + slot]};
+          ray.time = Q[Q_TMAX * N + slot];  // closest queries carry the ray time there
+        } else {
+          ray.o = a.pinhole ? cam_o : V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]};
+        }
       }
-      const int res = st0 >= ST_CLOSEST ? a.result[slot] : -1;
+      const int res = st0 >= ST_CLOSEST ? res_ld : -1;
       int px = 0, py = 0, sample = 0;
       // the pixel / sample coordinates (64-bit division, tile lookups) are only needed when a
       // sample starts; later steps continue its RNG stream from the stored key and counter
@@ -565,8 +592,8 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       rng.ctr = 0;
       bool fresh = false;  // a sample started in this step: its RNG key goes to the state
       if (st0 >= ST_CLOSEST) {
-        rng.key = (uint64_t)ld(F_KEY) | ((uint64_t)ld(F_KEY + 1) << 32);
-        rng.ctr = ld(F_RNG);
+        rng.key = (uint64_t)key_lo | ((uint64_t)key_hi << 32);
+        rng.ctr = rng_ctr;
       }
       bool retired = false;
       bool idle = unit == -2;
@@ -632,15 +659,6 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
             ret = V3{0.1f, 0.1f, 0.1f};
             returning = true;
           } else {
-            // hit attributes computed by the trace kernel (prim_hit<true> on this primitive)
-            const float* H = a.hit;
-            hp = V3{H[(HIT_P + 0) * N + slot], H[(HIT_P + 1) * N + slot], H[(HIT_P + 2) * N + slot]};
-            hn = V3{H[(HIT_N + 0) * N + slot], H[(HIT_N + 1) * N + slot], H[(HIT_N + 2) * N + slot]};
-            if (kTex) {
-              hu = H[HIT_U * N + slot];
-              hv = H[HIT_V * N + slot];
-            }
-            mat_id = (int)__float_as_uint(H[HIT_MAT * N + slot]);
             const rt_material& m = a.mats[mat_id];
             V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
             fin = V3{base.x * m.k_ambient, base.y * m.k_ambient, base.z * m.k_ambient};
@@ -652,6 +670,11 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
         } else if (st == ST_SHADOW) {
           if (res == 0) vis += 1.0f;
           ++ls;
+          if (light == 0) {  // final_color before any light: the ambient term (same ops as above)
+            const rt_material& m = a.mats[mat_id];
+            V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+            fin = V3{base.x * m.k_ambient, base.y * m.k_ambient, base.z * m.k_ambient};
+          }
           shade_now = true;
         }
         if (shade_now) {  // shade (raytracer.cpp:180-274)
@@ -831,28 +854,26 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
         stu(F_UNIT, (uint32_t)-2);
         a.query[Q_KIND * N + slot] = __int_as_float(-1);
       } else {
-        stu(F_UNIT, (uint32_t)unit);
+        if (fresh) stu(F_UNIT, (uint32_t)unit);  // a query without a new sample keeps its unit
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
-        stu(F_RNG, rng.ctr);
-        if (fresh) {
-          stu(F_KEY, (uint32_t)rng.key);
-          stu(F_KEY + 1, (uint32_t)(rng.key >> 32));
+        if (a.late_draws) {
+          stu(F_RNG, rng.ctr);
+          if (fresh) {
+            stu(F_KEY, (uint32_t)rng.key);
+            stu(F_KEY + 1, (uint32_t)(rng.key >> 32));
+          }
         }
         if (st == ST_SHADOW) {  // a closest query's ray travels in the query record
-          stu(F_LIGHT, (uint32_t)light);
-          stu(F_LS, (uint32_t)ls);
-          stf(F_VIS, vis);
-          stf(F_FIN, fin.x); stf(F_FIN + 1, fin.y); stf(F_FIN + 2, fin.z);
-          if (st0 != ST_SHADOW) {  // shadow -> shadow steps never change the ray or the hit
-            stf(F_RAY, ray.o.x); stf(F_RAY + 1, ray.o.y); stf(F_RAY + 2, ray.o.z);
-            stf(F_RAY + 3, ray.d.x); stf(F_RAY + 4, ray.d.y); stf(F_RAY + 5, ray.d.z);
-            stf(F_RAY + 6, ray.time);
-            stf(F_HP, hp.x); stf(F_HP + 1, hp.y); stf(F_HP + 2, hp.z);
-            stf(F_HN, hn.x); stf(F_HN + 1, hn.y); stf(F_HN + 2, hn.z);
-            stu(F_MAT, (uint32_t)mat_id);
-            if (kTex) {
-              stf(F_UV, hu);
-              stf(F_UV + 1, hv);
+          stu(F_LIGHT, (uint32_t)light | ((uint32_t)ls << 16));
+          if (ls > 0) stf(F_VIS, vis);
+          if (light > 0) { stf(F_FIN, fin.x); stf(F_FIN + 1, fin.y); stf(F_FIN + 2, fin.z); }
+          if (st0 != ST_SHADOW) {  // shadow -> shadow steps never change the ray
+            if (kFrames) {
+              stf(F_RAY, ray.o.x); stf(F_RAY + 1, ray.o.y); stf(F_RAY + 2, ray.o.z);
+              stf(F_RAY + 3, ray.d.x); stf(F_RAY + 4, ray.d.y); stf(F_RAY + 5, ray.d.z);
+              stf(F_RAY + 6, ray.time);
+            } else if (!a.pinhole) {
+              stf(F_RAY, ray.o.x); stf(F_RAY + 1, ray.o.y); stf(F_RAY + 2, ray.o.z);
             }
           }
         }
@@ -987,6 +1008,7 @@ struct rt_scene_s {
   void* d_prim_refs = nullptr;
   void* d_ref_boxes = nullptr;
   int n_cu = 0, trace_blocks_per_cu = 0;
+  bool late_draws = false;  // a light with radius > 0 or a rough material: draws after a sample's start
   int* d_spill = nullptr;
   size_t spill_cap = 0;
   // per-render workspace (grown on demand)
@@ -1073,7 +1095,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   if (d->prim_stride != 64 && d->prim_stride != 128)
     return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
   if (d->n_materials <= 0 || !d->materials) return fail(RT_EINVAL, "rt_scene_create: need >= 1 material");
-  if (d->n_lights < 0 || (d->n_lights > 0 && !d->lights)) return fail(RT_EINVAL, "rt_scene_create: bad lights");
+  if (d->n_lights < 0 || d->n_lights > 65535 || (d->n_lights > 0 && !d->lights))
+    return fail(RT_EINVAL, "rt_scene_create: bad lights (at most 65535)");
   // every node reference in range and pointing forward (the kernel follows them unchecked)
   const int64_t n_bounded = (int64_t)d->n_prims - d->n_unbounded;
   for (int32_t i = 0; i < d->n_nodes; ++i) {
@@ -1093,6 +1116,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   rt_scene_s* s = new rt_scene_s();
   s->device = device;
   s->desc = *d;
+  for (int i = 0; i < d->n_lights; ++i) s->late_draws = s->late_draws || d->lights[i].radius > 0.0f;
+  for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
   int rc = RT_OK;
   if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
       (rc = upload(&s->d_nodes, d->nodes, (size_t)d->n_nodes * sizeof(rt_node4))) ||
@@ -1135,7 +1160,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   if (tile_w <= 0 || tile_h <= 0 || tile_w % 8 || tile_h % 8)
     return fail(RT_EINVAL, "rt_render_tiles: tile size must be a positive multiple of 8");
   if (cam->res_x <= 0 || cam->res_y <= 0) return fail(RT_EINVAL, "rt_render_tiles: camera resolution is 0");
-  if (p->spp_sqrt > 4096 || p->light_samples < 0) return fail(RT_EINVAL, "rt_render_tiles: bad sample counts");
+  if (p->spp_sqrt > 4096 || p->light_samples < 0 || p->light_samples > 65535)
+    return fail(RT_EINVAL, "rt_render_tiles: bad sample counts (light_samples at most 65535)");
   const int tiles_x = (cam->res_x + tile_w - 1) / tile_w, tiles_y = (cam->res_y + tile_h - 1) / tile_h;
   for (int i = 0; i < n_tiles; ++i)
     if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(RT_EINVAL, "rt_render_tiles: tile id out of range");
@@ -1226,6 +1252,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.query = s->d_query;
   la.result = s->d_result;
   la.hit = s->d_hit;
+  la.late_draws = s->late_draws ? 1 : 0;
+  la.pinhole = cam->aperture <= 0.0f ? 1 : 0;
   la.any_query = ctl + 768;  // byte 3072
   la.batch_ctr = ctl + 64;  // byte 256
 
