@@ -66,7 +66,7 @@ def parse():
                     help="SURVEY.md 8(d) C2 BVH-stress variant: the soup without lights (one ray per sample)")
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="concurrent reference processes for the all-cores CPU figure (<= 1: skip)")
-    ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+    ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "r01_v13_pmc_traffic.json"),
                     help="JSON with per-launch HBM bytes of trace_kernel from rocprofv3 --pmc (tools/pmc_traffic.py)")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")

@@ -1044,7 +1044,7 @@ extern "C" {
 const char* rt_last_error(void) { return g_err.c_str(); }
 
 const char* rt_build_info(void) {
-  return "librt_hip: gfx950 hand-written HIP; wavefront logic+trace kernels; BVH2 + LDS stack; no MFMA";
+  return "librt_hip: gfx950 hand-written HIP; wavefront logic+trace kernels; SAH BVH4 (64-B quantised nodes) + LDS stack; no MFMA";
 }
 
 int rt_device_count(int32_t* count) {
