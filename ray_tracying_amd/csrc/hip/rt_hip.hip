@@ -142,6 +142,8 @@ struct TraceArgs {
   unsigned long long* counters;  // box tests, prim tests (count_work)
   float* hit;                 // [HIT_COUNT][n_slots]: attributes of a closest hit (for the logic step)
   int has_tex;                // some material is textured: hit u, v needed
+  int refill_min;             // refill kernel: refill finished lanes when fewer than this many traverse
+  int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
 };
 
 // ---------------------------------------------------------------- traversal
@@ -195,7 +197,10 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
     PrimA P;
     load_prim_a(rec, P);
     float t;
-    if (kCount) ++nprim;
+    if (kCount) {
+      ++nprim;
+      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) atomicAdd(a.counters + 61, 1ull);  // wave-level prim tests
+    }
     if (!prim_hit<false, kPlanesOnly>(P, rec, r, t, nullptr)) continue;
     const int2 ref = a.prim_refs[pi];
     auto leaf_ok = [&]() {
@@ -227,183 +232,187 @@ __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
   ca = c;
 }
 
-// 4 waves/SIMD (<= 128 VGPRs, no spills); 5 waves needs 96 VGPRs and spills in the leaf path
+// One query's traversal state between node steps.
+struct Query {
+  Ray r;
+  V3 inv;       // reciprocal direction for the culling slabs (|d| clamped away from 0)
+  float tmax;   // shadow: light distance
+  bool any;     // shadow query: any hit with t <= tmax
+  uint32_t par; // bit i: fabs(d_i) < 1e-6 (double), the exact slab's parallel test
+};
+
+// Reads slot's query record; false if the slot emitted no query this step.
+__device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query& q) {
+  const int N = a.n_slots;
+  const int kind = __float_as_int(a.query[Q_KIND * N + slot]);
+  if (kind < 0) return false;
+  q.r.o = V3{a.query[(Q_O + 0) * N + slot], a.query[(Q_O + 1) * N + slot], a.query[(Q_O + 2) * N + slot]};
+  q.r.d = V3{a.query[(Q_D + 0) * N + slot], a.query[(Q_D + 1) * N + slot], a.query[(Q_D + 2) * N + slot]};
+  const float tq = a.query[Q_TMAX * N + slot];
+  q.any = (kind & 1) != 0;
+  q.tmax = q.any ? tq : 0.0f;
+  q.r.time = q.any ? 0.0f : tq;  // shadow rays have time 0 (raytracer.cpp:225, shapes.hpp:28)
+  uint32_t par = 0;
+  par |= ((double)fabsf(q.r.d.x) < 1e-6) ? 1u : 0u;
+  par |= ((double)fabsf(q.r.d.y) < 1e-6) ? 2u : 0u;
+  par |= ((double)fabsf(q.r.d.z) < 1e-6) ? 4u : 0u;
+  q.par = par;
+  auto safe_inv = [](float d) {
+    float dd = fabsf(d) < 1e-12f ? copysignf(1e-12f, d) : d;
+    return 1.0f / dd;
+  };
+  q.inv = V3{safe_inv(q.r.d.x), safe_inv(q.r.d.y), safe_inv(q.r.d.z)};
+  return true;
+}
+
+// One 4-wide node visit: leaf children's primitives tested first, internal children pushed
+// far-to-near, `node` becomes the nearest one (or the popped stack top, or -1).
 template <bool kCount, bool kPlanesOnly>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void trace_kernel(TraceArgs ta) {
-  extern __shared__ __attribute__((aligned(16))) int lds_stack[];
-  const unsigned int nq = (unsigned)ta.n_slots;
-  const int lane = threadIdx.x & 63;
-  unsigned int nrays = 0;
-  const int gtid = blockIdx.x * kBlock + threadIdx.x;
-  unsigned int nbox = 0, nprim = 0;
-  unsigned long long dg_any_rays = 0, dg_any_box = 0;  // kCount diagnostics: shadow (any-hit) queries
-  const TraceArgs& a = ta;
-  const int N = ta.n_slots;
-  if (*ta.any_query == 0u) return;  // no slot emitted a query this step
-  // The slots are cut into kFetchShards slices with a counter each (one device-wide counter
-  // serialises at ~12 ns per 64-slot fetch: 1.6 ms per 8M-slot launch); a wave drains the
-  // slice of its block (blockIdx % 8 ~ its XCD) first, then helps the others.
-  const unsigned shard_len = (((nq + kFetchShards - 1) / kFetchShards) + 63u) & ~63u;
-  for (int sk = 0; sk < kFetchShards; ++sk) {
-   const int sh = (int)((blockIdx.x + sk) % kFetchShards);
-   const unsigned sh_start = (unsigned)sh * shard_len;
-   if (sh_start >= nq) continue;
-   const unsigned sh_len = min(shard_len, nq - sh_start);
-   unsigned int* ctr = ta.fetch + sh * kFetchStride;
-   for (;;) {  // persistent: each wave pulls 64 queries at a time
-    unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(ctr, 64u);
-    base = __shfl(base, 0);
-    if (base >= sh_len) break;
-    if (base + lane >= sh_len) continue;
-    const unsigned int qi = sh_start + base + lane;
-    const int slot = (int)qi;
-    const int kind = __float_as_int(ta.query[Q_KIND * N + slot]);
-    if (kind < 0) continue;  // no query from this slot in this step
-    ++nrays;
-    if (kCount && (kind & 1)) ++dg_any_rays;
-    Ray r;
-    r.o = V3{ta.query[(Q_O + 0) * N + slot], ta.query[(Q_O + 1) * N + slot], ta.query[(Q_O + 2) * N + slot]};
-    r.d = V3{ta.query[(Q_D + 0) * N + slot], ta.query[(Q_D + 1) * N + slot], ta.query[(Q_D + 2) * N + slot]};
-    const float tq = ta.query[Q_TMAX * N + slot];
-    const bool any = (kind & 1) != 0;
-    const float tmax = any ? tq : 0.0f;
-    r.time = any ? 0.0f : tq;  // shadow rays have time 0 (raytracer.cpp:225, shapes.hpp:28)
-    HitState h{__builtin_inff(), 0x7fffffff, -1, false};
-    uint32_t par = 0;
-    par |= ((double)fabsf(r.d.x) < 1e-6) ? 1u : 0u;
-    par |= ((double)fabsf(r.d.y) < 1e-6) ? 2u : 0u;
-    par |= ((double)fabsf(r.d.z) < 1e-6) ? 4u : 0u;
-    if (a.c.n_prims > 0 && !a.c.use_bvh) {  // BVH::intersect_linear (acceleration.cpp:124-139)
-      test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, r, any, tmax, par, false, h, nprim);
-    } else if (a.c.n_prims > 0) {
-      auto safe_inv = [](float d) {
-        float dd = fabsf(d) < 1e-12f ? copysignf(1e-12f, d) : d;
-        return 1.0f / dd;
-      };
-      const V3 inv{safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z)};
-      int* lstack = lds_stack + threadIdx.x;
-      int sp = 0;
-      int node = a.n_nodes > 0 ? 0 : -1;
-      while (node >= 0) {
-        // 64-B node, 8-bit child grids (rt_hip.h).  Slab entry/exit along x for child k:
-        // (origin + q*step - o) * inv == q * (step*inv) + (origin - o)*inv, evaluated as one
-        // packed fma per pair of children: culling only -- the boxes carry 1e-5*scale padding
-        // and every candidate hit is re-checked exactly (ref_leaf_ok + the primitive test).
-        const float4* nd = a.c.nodes + (size_t)node * 4;
-        const float4 g = nd[0];
-        const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
-        const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
-        const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
-        const uint32_t ex = __float_as_uint(g.w);
-        const uint32_t meta = qb.z;
-        const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
-        const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
-        const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
-        const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
-        const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
-        auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
-        auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };
-        const f32x2 t_lx01 = __builtin_elementwise_fma(lo2(qa.x), Bx, Ax), t_lx23 = __builtin_elementwise_fma(hi2(qa.x), Bx, Ax);
-        const f32x2 t_hx01 = __builtin_elementwise_fma(lo2(qa.y), Bx, Ax), t_hx23 = __builtin_elementwise_fma(hi2(qa.y), Bx, Ax);
-        const f32x2 t_ly01 = __builtin_elementwise_fma(lo2(qa.z), By, Ay), t_ly23 = __builtin_elementwise_fma(hi2(qa.z), By, Ay);
-        const f32x2 t_hy01 = __builtin_elementwise_fma(lo2(qa.w), By, Ay), t_hy23 = __builtin_elementwise_fma(hi2(qa.w), By, Ay);
-        const f32x2 t_lz01 = __builtin_elementwise_fma(lo2(qb.x), Bz, Az), t_lz23 = __builtin_elementwise_fma(hi2(qb.x), Bz, Az);
-        const f32x2 t_hz01 = __builtin_elementwise_fma(lo2(qb.y), Bz, Az), t_hz23 = __builtin_elementwise_fma(hi2(qb.y), Bz, Az);
-        const float tx1[4] = {t_lx01.x, t_lx01.y, t_lx23.x, t_lx23.y}, tx2[4] = {t_hx01.x, t_hx01.y, t_hx23.x, t_hx23.y};
-        const float ty1[4] = {t_ly01.x, t_ly01.y, t_ly23.x, t_ly23.y}, ty2[4] = {t_hy01.x, t_hy01.y, t_hy23.x, t_hy23.y};
-        const float tz1[4] = {t_lz01.x, t_lz01.y, t_lz23.x, t_lz23.y}, tz2[4] = {t_hz01.x, t_hz01.y, t_hz23.x, t_hz23.y};
-        float tn[4];
-        bool hit[4];
+__device__ __forceinline__ void node_step(const TraceArgs& a, const Query& q, HitState& h, int& node, int& sp,
+                                          int* lstack, int gtid, unsigned int& nbox, unsigned int& nprim,
+                                          unsigned long long& dg_any_box, unsigned int& nvisit) {
+  const Ray& r = q.r;
+  const V3& inv = q.inv;
+  const bool any = q.any;
+  const float tmax = q.tmax;
+  // 64-B node, 8-bit child grids (rt_hip.h).  Slab entry/exit along x for child k:
+  // (origin + q*step - o) * inv == q * (step*inv) + (origin - o)*inv, evaluated as one
+  // packed fma per pair of children: culling only -- the boxes carry 1e-5*scale padding
+  // and every candidate hit is re-checked exactly (ref_leaf_ok + the primitive test).
+  const float4* nd = a.c.nodes + (size_t)node * 4;
+  const float4 g = nd[0];
+  const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
+  const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
+  const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
+  const uint32_t ex = __float_as_uint(g.w);
+  const uint32_t meta = qb.z;
+  const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
+  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
+  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
+  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
+  const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
+  auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
+  auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };
+  const f32x2 t_lx01 = __builtin_elementwise_fma(lo2(qa.x), Bx, Ax), t_lx23 = __builtin_elementwise_fma(hi2(qa.x), Bx, Ax);
+  const f32x2 t_hx01 = __builtin_elementwise_fma(lo2(qa.y), Bx, Ax), t_hx23 = __builtin_elementwise_fma(hi2(qa.y), Bx, Ax);
+  const f32x2 t_ly01 = __builtin_elementwise_fma(lo2(qa.z), By, Ay), t_ly23 = __builtin_elementwise_fma(hi2(qa.z), By, Ay);
+  const f32x2 t_hy01 = __builtin_elementwise_fma(lo2(qa.w), By, Ay), t_hy23 = __builtin_elementwise_fma(hi2(qa.w), By, Ay);
+  const f32x2 t_lz01 = __builtin_elementwise_fma(lo2(qb.x), Bz, Az), t_lz23 = __builtin_elementwise_fma(hi2(qb.x), Bz, Az);
+  const f32x2 t_hz01 = __builtin_elementwise_fma(lo2(qb.y), Bz, Az), t_hz23 = __builtin_elementwise_fma(hi2(qb.y), Bz, Az);
+  const float tx1[4] = {t_lx01.x, t_lx01.y, t_lx23.x, t_lx23.y}, tx2[4] = {t_hx01.x, t_hx01.y, t_hx23.x, t_hx23.y};
+  const float ty1[4] = {t_ly01.x, t_ly01.y, t_ly23.x, t_ly23.y}, ty2[4] = {t_hy01.x, t_hy01.y, t_hy23.x, t_hy23.y};
+  const float tz1[4] = {t_lz01.x, t_lz01.y, t_lz23.x, t_lz23.y}, tz2[4] = {t_hz01.x, t_hz01.y, t_hz23.x, t_hz23.y};
+  float tn[4];
+  bool hit[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float n0 = fmaxf(fmaxf(fminf(tx1[k], tx2[k]), fminf(ty1[k], ty2[k])), fminf(tz1[k], tz2[k]));
-          const float f0 = fminf(fminf(fmaxf(tx1[k], tx2[k]), fmaxf(ty1[k], ty2[k])), fmaxf(tz1[k], tz2[k]));
-          tn[k] = n0;
-          hit[k] = ((meta >> (8 * k)) & 0xffu) != 0 && n0 <= f0 && f0 >= 0.0f;
-        }
-        if (kCount) nbox += __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
-                                                (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
-        if (kCount && any) dg_any_box += __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
-                                                              (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
-        // leaves first (their hits tighten the bound before internal children are ordered);
-        // one primitive-test instance walks the leaf bitmask (no 4x inlined copies)
-        uint32_t leaves = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (hit[k] && ((meta >> (8 * k)) & 0x80u)) {
-            leaves |= 1u << k;
-            hit[k] = false;
-          }
-        }
-        while (leaves != 0u) {
-          const int k = __builtin_ctz(leaves);
-          leaves &= leaves - 1u;
-          const float tk = k == 0 ? tn[0] : k == 1 ? tn[1] : k == 2 ? tn[2] : tn[3];
-          const int ck = k == 0 ? cc[0] : k == 1 ? cc[1] : k == 2 ? cc[2] : cc[3];
-          float lim = any ? tmax : h.best_t;
-          lim = lim + (lim * 1e-5f + a.c.eps_abs);
-          if (!(tk > lim)) test_prims<kCount, kPlanesOnly>(a, ck, (int)((meta >> (8 * k)) & 0x7fu), r, any, tmax, par, true, h, nprim);
-          if (h.done) break;
-        }
-        if (h.done) break;
-        float lim = any ? tmax : h.best_t;
-        lim = lim + (lim * 1e-5f + a.c.eps_abs);
-        float t0 = __builtin_inff(), t1 = __builtin_inff(), t2 = __builtin_inff(), t3 = __builtin_inff();
-        int c0 = -1, c1 = -1, c2 = -1, c3 = -1;
-        if (hit[0] && !(tn[0] > lim)) { t0 = tn[0]; c0 = cc[0]; }
-        if (hit[1] && !(tn[1] > lim)) { t1 = tn[1]; c1 = cc[1]; }
-        if (hit[2] && !(tn[2] > lim)) { t2 = tn[2]; c2 = cc[2]; }
-        if (hit[3] && !(tn[3] > lim)) { t3 = tn[3]; c3 = cc[3]; }
-        // sort 4 (t, child) ascending; misses (-1, inf) sink to the end
-        cswap(t0, c0, t1, c1);
-        cswap(t2, c2, t3, c3);
-        cswap(t0, c0, t2, c2);
-        cswap(t1, c1, t3, c3);
-        cswap(t1, c1, t2, c2);
-        auto push = [&](int v) {
-          if (sp < a.lds_entries) lstack[sp * kBlock] = v;
-          else a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = v;
-          ++sp;
-        };
-        if (c3 >= 0) push(c3);
-        if (c2 >= 0) push(c2);
-        if (c1 >= 0) push(c1);
-        if (c0 >= 0) {
-          node = c0;
-        } else if (sp > 0) {
-          --sp;
-          node = sp < a.lds_entries ? lstack[sp * kBlock] : a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid];
-        } else {
-          node = -1;
-        }
-      }
-      // primitives whose accepted region is not boxable: tested by every ray
-      if (!h.done && a.n_unbounded > 0)
-        test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, any, tmax, par, true, h, nprim);
-    }
-    ta.result[slot] = any ? (h.done ? 1 : 0) : h.best_idx;
-    if (!any && h.best_idx >= 0) {
-      // the hit record the Trace/shade step needs (raytracer.cpp:293-303): the same
-      // primitive test with attributes, on the primitive this lane just tested (cached)
-      const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
-      PrimA P;
-      load_prim_a(rec, P);
-      HitAttr at;
-      float t;
-      if (ta.has_tex) prim_hit<true, kPlanesOnly, true>(P, rec, r, t, &at);
-      else prim_hit<true, kPlanesOnly, false>(P, rec, r, t, &at);
-      float* H = ta.hit;
-      H[(HIT_P + 0) * N + slot] = at.p.x; H[(HIT_P + 1) * N + slot] = at.p.y; H[(HIT_P + 2) * N + slot] = at.p.z;
-      H[(HIT_N + 0) * N + slot] = at.n.x; H[(HIT_N + 1) * N + slot] = at.n.y; H[(HIT_N + 2) * N + slot] = at.n.z;
-      if (ta.has_tex) {
-        H[HIT_U * N + slot] = at.u;
-        H[HIT_V * N + slot] = at.v;
-      }
-      H[HIT_MAT * N + slot] = __uint_as_float(RT_TAG_MATERIAL(prim_tag(P)));
-    }
-   }
+  for (int k = 0; k < 4; ++k) {
+    const float n0 = fmaxf(fmaxf(fminf(tx1[k], tx2[k]), fminf(ty1[k], ty2[k])), fminf(tz1[k], tz2[k]));
+    const float f0 = fminf(fminf(fmaxf(tx1[k], tx2[k]), fmaxf(ty1[k], ty2[k])), fmaxf(tz1[k], tz2[k]));
+    tn[k] = n0;
+    hit[k] = ((meta >> (8 * k)) & 0xffu) != 0 && n0 <= f0 && f0 >= 0.0f;
   }
+  if (kCount) {
+    const uint64_t wm = __ballot(1);
+    if (__lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
+    ++nvisit;
+    const unsigned nb = __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
+                                            (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
+    nbox += nb;
+    if (any) dg_any_box += nb;
+  }
+  // leaves first (their hits tighten the bound before internal children are ordered);
+  // one primitive-test instance walks the leaf bitmask (no 4x inlined copies)
+  uint32_t leaves = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (hit[k] && ((meta >> (8 * k)) & 0x80u)) {
+      leaves |= 1u << k;
+      hit[k] = false;
+    }
+  }
+  while (leaves != 0u) {
+    const int k = __builtin_ctz(leaves);
+    leaves &= leaves - 1u;
+    const float tk = k == 0 ? tn[0] : k == 1 ? tn[1] : k == 2 ? tn[2] : tn[3];
+    const int ck = k == 0 ? cc[0] : k == 1 ? cc[1] : k == 2 ? cc[2] : cc[3];
+    float lim = any ? tmax : h.best_t;
+    lim = lim + (lim * 1e-5f + a.c.eps_abs);
+    if (!(tk > lim))
+      test_prims<kCount, kPlanesOnly>(a, ck, (int)((meta >> (8 * k)) & 0x7fu), r, any, tmax, q.par, true, h, nprim);
+    if (h.done) break;
+  }
+  if (h.done) {
+    node = -1;
+    return;
+  }
+  float lim = any ? tmax : h.best_t;
+  lim = lim + (lim * 1e-5f + a.c.eps_abs);
+  float t0 = __builtin_inff(), t1 = __builtin_inff(), t2 = __builtin_inff(), t3 = __builtin_inff();
+  int c0 = -1, c1 = -1, c2 = -1, c3 = -1;
+  if (hit[0] && !(tn[0] > lim)) { t0 = tn[0]; c0 = cc[0]; }
+  if (hit[1] && !(tn[1] > lim)) { t1 = tn[1]; c1 = cc[1]; }
+  if (hit[2] && !(tn[2] > lim)) { t2 = tn[2]; c2 = cc[2]; }
+  if (hit[3] && !(tn[3] > lim)) { t3 = tn[3]; c3 = cc[3]; }
+  // sort 4 (t, child) ascending; misses (-1, inf) sink to the end
+  cswap(t0, c0, t1, c1);
+  cswap(t2, c2, t3, c3);
+  cswap(t0, c0, t2, c2);
+  cswap(t1, c1, t3, c3);
+  cswap(t1, c1, t2, c2);
+  auto push = [&](int v) {
+    if (sp < a.lds_entries) lstack[sp * kBlock] = v;
+    else a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = v;
+    ++sp;
+  };
+  if (c3 >= 0) push(c3);
+  if (c2 >= 0) push(c2);
+  if (c1 >= 0) push(c1);
+  if (c0 >= 0) {
+    node = c0;
+  } else if (sp > 0) {
+    --sp;
+    node = sp < a.lds_entries ? lstack[sp * kBlock] : a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid];
+  } else {
+    node = -1;
+  }
+}
+
+// After the traversal: the primitives whose region could not be boxed, then the result
+// word and (closest hits) the hit record the logic step shades.
+template <bool kCount, bool kPlanesOnly>
+__device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const Query& q, HitState& h,
+                                             unsigned int& nprim) {
+  const int N = a.n_slots;
+  const Ray& r = q.r;
+  // primitives whose accepted region is not boxable: tested by every ray
+  if (a.c.use_bvh && !h.done && a.n_unbounded > 0)
+    test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, q.any, q.tmax, q.par, true, h, nprim);
+  a.result[slot] = q.any ? (h.done ? 1 : 0) : h.best_idx;
+  if (!q.any && h.best_idx >= 0) {
+    // the hit record the Trace/shade step needs (raytracer.cpp:293-303): the same
+    // primitive test with attributes, on the primitive this lane just tested (cached)
+    const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
+    PrimA P;
+    load_prim_a(rec, P);
+    HitAttr at;
+    float t;
+    if (a.has_tex) prim_hit<true, kPlanesOnly, true>(P, rec, r, t, &at);
+    else prim_hit<true, kPlanesOnly, false>(P, rec, r, t, &at);
+    float* H = a.hit;
+    H[(HIT_P + 0) * N + slot] = at.p.x; H[(HIT_P + 1) * N + slot] = at.p.y; H[(HIT_P + 2) * N + slot] = at.p.z;
+    H[(HIT_N + 0) * N + slot] = at.n.x; H[(HIT_N + 1) * N + slot] = at.n.y; H[(HIT_N + 2) * N + slot] = at.n.z;
+    if (a.has_tex) {
+      H[HIT_U * N + slot] = at.u;
+      H[HIT_V * N + slot] = at.v;
+    }
+    H[HIT_MAT * N + slot] = __uint_as_float(RT_TAG_MATERIAL(prim_tag(P)));
+  }
+}
+
+template <bool kCount>
+__device__ __forceinline__ void trace_counters_out(const TraceArgs& ta, int lane, unsigned int nrays, unsigned int nbox,
+                                                   unsigned int nprim, unsigned long long dg_any_rays,
+                                                   unsigned long long dg_any_box, unsigned int nvisit) {
   unsigned long long nr = nrays;
   for (int off = 32; off > 0; off >>= 1) nr += __shfl_xor(nr, off);
   if (lane == 0 && nr) atomicAdd(ta.rays, nr);
@@ -421,11 +430,290 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
       dg_any_rays += __shfl_xor(dg_any_rays, off);
       dg_any_box += __shfl_xor(dg_any_box, off);
     }
+    unsigned long long v = nvisit;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if (lane == 0) {  // ctl byte 512
       atomicAdd(ta.counters + 62, dg_any_rays);
       atomicAdd(ta.counters + 63, dg_any_box);
+      atomicAdd(ta.counters + 59, v);  // lane-level node visits
     }
   }
+}
+
+// Batch kernel: a wave traces 64 consecutive slots to completion, then pulls the next 64.
+// 4 waves/SIMD (<= 128 VGPRs, no spills); 5 waves needs 96 VGPRs and spills in the leaf path
+template <bool kCount, bool kPlanesOnly>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void trace_kernel(TraceArgs ta) {
+  extern __shared__ __attribute__((aligned(16))) int lds_stack[];
+  const unsigned int nq = (unsigned)ta.n_slots;
+  const int lane = threadIdx.x & 63;
+  unsigned int nrays = 0;
+  const int gtid = blockIdx.x * kBlock + threadIdx.x;
+  unsigned int nbox = 0, nprim = 0, nvisit = 0;
+  unsigned long long dg_any_rays = 0, dg_any_box = 0;  // kCount diagnostics: shadow (any-hit) queries
+  const TraceArgs& a = ta;
+  if (*ta.any_query == 0u) return;  // no slot emitted a query this step
+  // The slots are cut into kFetchShards slices with a counter each (one device-wide counter
+  // serialises at ~12 ns per 64-slot fetch: 1.6 ms per 8M-slot launch); a wave drains the
+  // slice of its block (blockIdx % 8 ~ its XCD) first, then helps the others.
+  const unsigned shard_len = (((nq + kFetchShards - 1) / kFetchShards) + 63u) & ~63u;
+  for (int sk = 0; sk < kFetchShards; ++sk) {
+   const int sh = (int)((blockIdx.x + sk) % kFetchShards);
+   const unsigned sh_start = (unsigned)sh * shard_len;
+   if (sh_start >= nq) continue;
+   const unsigned sh_len = min(shard_len, nq - sh_start);
+   unsigned int* ctr = ta.fetch + sh * kFetchStride;
+   for (;;) {  // persistent: each wave pulls 64 queries at a time
+    unsigned int base = 0;
+    if (lane == 0) base = atomicAdd(ctr, 64u);
+    base = __shfl(base, 0);
+    if (base >= sh_len) break;
+    if (base + lane >= sh_len) continue;
+    const int slot = (int)(sh_start + base + lane);
+    Query q;
+    if (!begin_query(a, slot, q)) continue;  // no query from this slot in this step
+    ++nrays;
+    if (kCount && q.any) ++dg_any_rays;
+    HitState h{__builtin_inff(), 0x7fffffff, -1, false};
+    if (a.c.n_prims > 0 && !a.c.use_bvh) {  // BVH::intersect_linear (acceleration.cpp:124-139)
+      test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
+    } else if (a.c.n_prims > 0) {
+      int* lstack = lds_stack + threadIdx.x;
+      int sp = 0;
+      int node = a.n_nodes > 0 ? 0 : -1;
+      while (node >= 0) node_step<kCount, kPlanesOnly>(a, q, h, node, sp, lstack, gtid, nbox, nprim, dg_any_box, nvisit);
+    }
+    finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+   }
+  }
+  trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
+}
+
+// ---- refill kernel with postponed leaves
+// Stack / item entries: a node index (>= 0), a leaf = kLeafBit | first << 7 | count (first <
+// 2^24, count < 128), or kNoItem.  Each stack entry carries its t_near so it is re-culled
+// against the bound current when it is popped.
+constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr int kNoItem = -1;
+__device__ __forceinline__ bool is_leaf_item(int e) { return e != kNoItem && e < 0; }
+
+struct LaneStack {
+  int2* e;     // LDS (entry, t_near bits), lane-minor: e[i * kBlock]
+  int2* spill; // entries past lds_entries: spill[(i - lds) * n_threads + gtid]
+};
+
+__device__ __forceinline__ void stack_push(const TraceArgs& a, const LaneStack& S, int& sp, int gtid, int e, float t) {
+  if (sp < a.lds_entries) S.e[sp * kBlock] = make_int2(e, __float_as_int(t));
+  else S.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = make_int2(e, __float_as_int(t));
+  ++sp;
+}
+
+// Pops entries until one is still within the bound (each popped entry is re-culled against
+// the bound current now); kNoItem when the stack empties.  Wave-uniform fast path when no
+// lane's stack reaches into the HBM spill area.
+__device__ __forceinline__ int stack_pop_live(const TraceArgs& a, const LaneStack& S, int& sp, int gtid, float lim) {
+  if (__ballot(sp > a.lds_entries) == 0ull) {
+    while (sp > 0) {
+      --sp;
+      const int2 v = S.e[sp * kBlock];
+      if (!(__int_as_float(v.y) > lim)) return v.x;
+    }
+    return kNoItem;
+  }
+  while (sp > 0) {
+    --sp;
+    const int2 v = sp < a.lds_entries ? S.e[sp * kBlock] : S.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid];
+    if (!(__int_as_float(v.y) > lim)) return v.x;
+  }
+  return kNoItem;
+}
+
+__device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, const HitState& h) {
+  const float lim = q.any ? q.tmax : h.best_t;
+  return lim + (lim * 1e-5f + a.c.eps_abs);
+}
+
+// One 4-wide node visit: every child box the ray enters within the bound -- internal nodes
+// and leaves alike -- is ordered by t_near; the three farthest are pushed, the nearest
+// becomes the lane's item (a leaf item waits for the next leaf phase).
+template <bool kCount>
+__device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, const HitState& h, int node,
+                                          const LaneStack& S, int& sp, int gtid, unsigned int& nbox,
+                                          unsigned long long& dg_any_box, unsigned int& nvisit) {
+  const Ray& r = q.r;
+  const V3& inv = q.inv;
+  const float4* nd = a.c.nodes + (size_t)node * 4;
+  const float4 g = nd[0];
+  const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
+  const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
+  const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
+  const uint32_t ex = __float_as_uint(g.w);
+  const uint32_t meta = qb.z;
+  const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
+  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
+  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
+  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
+  const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
+  auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
+  auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };
+  const f32x2 t_lx01 = __builtin_elementwise_fma(lo2(qa.x), Bx, Ax), t_lx23 = __builtin_elementwise_fma(hi2(qa.x), Bx, Ax);
+  const f32x2 t_hx01 = __builtin_elementwise_fma(lo2(qa.y), Bx, Ax), t_hx23 = __builtin_elementwise_fma(hi2(qa.y), Bx, Ax);
+  const f32x2 t_ly01 = __builtin_elementwise_fma(lo2(qa.z), By, Ay), t_ly23 = __builtin_elementwise_fma(hi2(qa.z), By, Ay);
+  const f32x2 t_hy01 = __builtin_elementwise_fma(lo2(qa.w), By, Ay), t_hy23 = __builtin_elementwise_fma(hi2(qa.w), By, Ay);
+  const f32x2 t_lz01 = __builtin_elementwise_fma(lo2(qb.x), Bz, Az), t_lz23 = __builtin_elementwise_fma(hi2(qb.x), Bz, Az);
+  const f32x2 t_hz01 = __builtin_elementwise_fma(lo2(qb.y), Bz, Az), t_hz23 = __builtin_elementwise_fma(hi2(qb.y), Bz, Az);
+  const float tx1[4] = {t_lx01.x, t_lx01.y, t_lx23.x, t_lx23.y}, tx2[4] = {t_hx01.x, t_hx01.y, t_hx23.x, t_hx23.y};
+  const float ty1[4] = {t_ly01.x, t_ly01.y, t_ly23.x, t_ly23.y}, ty2[4] = {t_hy01.x, t_hy01.y, t_hy23.x, t_hy23.y};
+  const float tz1[4] = {t_lz01.x, t_lz01.y, t_lz23.x, t_lz23.y}, tz2[4] = {t_hz01.x, t_hz01.y, t_hz23.x, t_hz23.y};
+  if (kCount) {
+    const uint64_t wm = __ballot(1);
+    if (__lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
+    ++nvisit;
+    const unsigned nb = __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
+                                            (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
+    nbox += nb;
+    if (q.any) dg_any_box += nb;
+  }
+  const float lim = cull_limit(a, q, h);
+  float t[4];
+  int c[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float n0 = fmaxf(fmaxf(fminf(tx1[k], tx2[k]), fminf(ty1[k], ty2[k])), fminf(tz1[k], tz2[k]));
+    const float f0 = fminf(fminf(fmaxf(tx1[k], tx2[k]), fmaxf(ty1[k], ty2[k])), fmaxf(tz1[k], tz2[k]));
+    const uint32_t m = (meta >> (8 * k)) & 0xffu;
+    const bool hit = m != 0u && n0 <= f0 && f0 >= 0.0f && !(n0 > lim);
+    const int e = (m & 0x80u) ? (int)(kLeafBit | ((uint32_t)cc[k] << 7) | (m & 0x7fu)) : cc[k];
+    t[k] = hit ? n0 : __builtin_inff();
+    c[k] = hit ? e : kNoItem;
+  }
+  // sort 4 (t, entry) ascending; misses (kNoItem, inf) sink to the end
+  cswap(t[0], c[0], t[1], c[1]);
+  cswap(t[2], c[2], t[3], c[3]);
+  cswap(t[0], c[0], t[2], c[2]);
+  cswap(t[1], c[1], t[3], c[3]);
+  cswap(t[1], c[1], t[2], c[2]);
+  // push the three farther children far-to-near.  The valid entries are a prefix of the
+  // sorted four, so unconditional writes at sp, sp+v3, sp+v3+v2 leave exactly the valid ones
+  // below the new top (an invalid one lands on the top slot and is overwritten or abandoned).
+  if (__ballot(sp + 3 > a.lds_entries) == 0ull) {
+    const int v3 = c[3] != kNoItem, v2 = c[2] != kNoItem, v1 = c[1] != kNoItem;
+    int2* st = S.e + sp * kBlock;
+    st[0] = make_int2(c[3], __float_as_int(t[3]));
+    st[v3 * kBlock] = make_int2(c[2], __float_as_int(t[2]));
+    st[(v3 + v2) * kBlock] = make_int2(c[1], __float_as_int(t[1]));
+    sp += v3 + v2 + v1;
+  } else {
+    if (c[3] != kNoItem) stack_push(a, S, sp, gtid, c[3], t[3]);
+    if (c[2] != kNoItem) stack_push(a, S, sp, gtid, c[2], t[2]);
+    if (c[1] != kNoItem) stack_push(a, S, sp, gtid, c[1], t[1]);
+  }
+  if (c[0] != kNoItem) return c[0];
+  return stack_pop_live(a, S, sp, gtid, lim);
+}
+
+// Refill kernel.  Lanes that finished their query are handed new slots (from the wave's
+// current 64-slot range, then the next one) whenever fewer than `refill_min` lanes of the
+// wave still hold a query, so wave instructions keep most lanes busy instead of waiting for
+// the longest traversal of a fixed batch; write-back of finished queries is batched into the
+// same step.  Leaves are postponed: a lane whose nearest item is a leaf waits until at least
+// `leaf_min` lanes wait on one (or no lane has a node to visit), then they all test their
+// leaf's primitives together -- leaf hits are sparse (~1 per 8 node visits per lane), and
+// testing them at once keeps the primitive code from running with a handful of lanes.
+template <bool kCount, bool kPlanesOnly>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void trace_refill_kernel(TraceArgs ta) {
+  extern __shared__ __attribute__((aligned(16))) int lds_stack[];
+  const unsigned int nq = (unsigned)ta.n_slots;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lane_lt = (1ull << lane) - 1ull;
+  unsigned int nrays = 0;
+  const int gtid = blockIdx.x * kBlock + threadIdx.x;
+  unsigned int nbox = 0, nprim = 0, nvisit = 0;
+  unsigned long long dg_any_rays = 0, dg_any_box = 0;
+  const TraceArgs& a = ta;
+  if (*ta.any_query == 0u) return;
+  const unsigned shard_len = (((nq + kFetchShards - 1) / kFetchShards) + 63u) & ~63u;
+  // wave-uniform work queue: [q_next, q_end)
+  int sk = 0;
+  unsigned q_next = 0, q_end = 0;
+  bool exhausted = false;
+  // lane state
+  int slot = -1;        // query owned by this lane (traversing, or finished awaiting write-back)
+  int item = kNoItem;   // node to visit / leaf to test next; kNoItem: traversal finished
+  Query q;
+  HitState h{__builtin_inff(), 0x7fffffff, -1, false};
+  int sp = 0;
+  const LaneStack S{reinterpret_cast<int2*>(lds_stack) + threadIdx.x, reinterpret_cast<int2*>(a.spill)};
+  for (;;) {
+    uint64_t act = __ballot(item != kNoItem);
+    if (__popcll(act) < a.refill_min) {
+      if (slot >= 0 && item == kNoItem) {
+        finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+        slot = -1;
+      }
+      while (!exhausted) {
+        const uint64_t freem = __ballot(slot < 0);
+        if (freem == 0ull) break;
+        if (q_next >= q_end) {  // next 64 slots: this shard's counter, then the other shards'
+          for (;;) {
+            const int sh = (int)((blockIdx.x + sk) % kFetchShards);
+            const unsigned st0 = (unsigned)sh * shard_len;
+            const unsigned len = st0 < nq ? min(shard_len, nq - st0) : 0u;
+            unsigned base = 0;
+            if (len > 0) {
+              if (lane == 0) base = atomicAdd(ta.fetch + sh * kFetchStride, 64u);
+              base = __shfl(base, 0);
+            }
+            if (len > 0 && base < len) {
+              q_next = st0 + base;
+              q_end = st0 + min(base + 64u, len);
+              break;
+            }
+            if (++sk >= kFetchShards) {
+              exhausted = true;
+              break;
+            }
+          }
+          if (exhausted) break;
+        }
+        const unsigned rank = (unsigned)__popcll(freem & lane_lt);
+        const unsigned avail = q_end - q_next;
+        if (slot < 0 && rank < avail) {
+          const int s = (int)(q_next + rank);
+          if (begin_query(a, s, q)) {
+            slot = s;
+            ++nrays;
+            if (kCount && q.any) ++dg_any_rays;
+            h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
+            sp = 0;
+            item = (a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem;
+            if (a.c.n_prims > 0 && !a.c.use_bvh)  // BVH::intersect_linear (acceleration.cpp:124-139)
+              test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
+            if (item == kNoItem) {  // nothing to traverse: write back at once
+              finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+              slot = -1;
+            }
+          }
+        }
+        q_next += min(avail, (unsigned)__popcll(freem));
+      }
+      act = __ballot(item != kNoItem);
+      if (act == 0ull && exhausted) break;
+    }
+    // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
+    const uint64_t leafm = __ballot(is_leaf_item(item));
+    if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+      if (is_leaf_item(item)) {
+        const uint32_t e = (uint32_t)item;
+        test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
+                                        true, h, nprim);
+        item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, cull_limit(a, q, h));
+      }
+    }
+    // node phase
+    if (item >= 0) item = node_visit<kCount>(a, q, h, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+  }
+  trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
 }
 
 // ---------------------------------------------------------------- shading helpers
@@ -964,6 +1252,41 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
   if (planes) hipLaunchKernelGGL((logic_kernel<F, T, true>), dim3(blocks), dim3(kBlock), 0, st, la);
   else hipLaunchKernelGGL((logic_kernel<F, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
 }
+// trace launch: the refill kernel (default) or the fixed-batch kernel (RT_REFILL=0)
+void launch_trace(const TraceArgs& ta, bool count, bool planes, unsigned blocks, size_t lds, hipStream_t st) {
+  if (ta.refill_min > 0) {
+    if (count) {
+      if (planes) hipLaunchKernelGGL((trace_refill_kernel<true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+      else hipLaunchKernelGGL((trace_refill_kernel<true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    } else {
+      if (planes) hipLaunchKernelGGL((trace_refill_kernel<false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+      else hipLaunchKernelGGL((trace_refill_kernel<false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    }
+  } else {
+    if (count) {
+      if (planes) hipLaunchKernelGGL((trace_kernel<true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+      else hipLaunchKernelGGL((trace_kernel<true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    } else {
+      if (planes) hipLaunchKernelGGL((trace_kernel<false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+      else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    }
+  }
+}
+static int leaf_min_env() {
+  static const int v = [] {
+    const char* e = std::getenv("RT_LEAF_MIN");
+    return e ? std::max(1, std::min(64, std::atoi(e))) : 16;
+  }();
+  return v;
+}
+static int refill_min_env() {
+  static const int v = [] {
+    const char* e = std::getenv("RT_REFILL");
+    return e ? std::max(0, std::min(64, std::atoi(e))) : 48;
+  }();
+  return v;
+}
+
 void launch_logic(const LogicArgs& la, bool frames, bool tex, bool planes, unsigned blocks, hipStream_t st) {
   if (frames) {
     if (tex) launch_logic2<true, true>(la, planes, blocks, st);
@@ -1140,8 +1463,12 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const int lds_entries = std::min(d->stack_bound, lds_stack_entries());
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, (d->prim_stride == 64 ? trace_kernel<false, true> : trace_kernel<false, false>), kBlock,
-                                                     (size_t)lds_entries * kBlock * sizeof(int)) != hipSuccess || bpc < 1)
+    const bool refill = d->n_prims < (1 << 24) && refill_min_env() > 0;
+    const bool planes = d->prim_stride == 64;
+    const void* fn = refill ? (planes ? (const void*)trace_refill_kernel<false, true> : (const void*)trace_refill_kernel<false, false>)
+                            : (planes ? (const void*)trace_kernel<false, true> : (const void*)trace_kernel<false, false>);
+    const size_t lds_bytes = (size_t)lds_entries * kBlock * (refill ? 2 * sizeof(int) : sizeof(int));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kBlock, lds_bytes) != hipSuccess || bpc < 1)
       bpc = 2;
     s->n_cu = ncu;
     s->trace_blocks_per_cu = bpc;
@@ -1272,6 +1599,9 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries());
+  // the refill kernel's leaf items hold first << 7 in 31 bits
+  ta.refill_min = s->desc.n_prims < (1 << 24) ? refill_min_env() : 0;
+  ta.leaf_min = leaf_min_env();
   const unsigned trace_blocks = (unsigned)std::max(1, std::min(s->n_cu * s->trace_blocks_per_cu,
                                                                (n_slots + kBlock - 1) / kBlock));
   ta.n_threads = (int)trace_blocks * kBlock;
@@ -1280,12 +1610,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     if (s->d_spill) (void)hipFree(s->d_spill);
     s->d_spill = nullptr;
     s->spill_cap = 0;
-    HIP_TRY(hipMalloc(&s->d_spill, (size_t)spill_entries * ta.n_threads * sizeof(int)), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_spill, (size_t)spill_entries * ta.n_threads * sizeof(int2)), RT_ENOMEM);
     s->spill_cap = (size_t)spill_entries * ta.n_threads;
   }
   ta.spill = s->d_spill;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
-  const size_t lds = (size_t)ta.lds_entries * kBlock * sizeof(int);
+  // refill kernel: entry + t_near per stack slot
+  const size_t lds = (size_t)ta.lds_entries * kBlock * (ta.refill_min > 0 ? 2 * sizeof(int) : sizeof(int));
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result,
@@ -1307,13 +1638,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipMemcpyAsync(s->h_flag, ctl + 768, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
-    if (p->count_work) {
-      if (planes_only) hipLaunchKernelGGL((trace_kernel<true, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
-      else hipLaunchKernelGGL((trace_kernel<true, false>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
-    } else {
-      if (planes_only) hipLaunchKernelGGL((trace_kernel<false, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
-      else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
-    }
+    launch_trace(ta, p->count_work != 0, planes_only, trace_blocks, lds, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
     HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
@@ -1328,8 +1653,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       for (int k = 0; k < replay_reps; ++k) {
         HIP_TRY(hipMemsetAsync(ctl + 512, 0, kFetchShards * kFetchStride * 4, stream), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
-        if (planes_only) hipLaunchKernelGGL((trace_kernel<false, true>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
-        else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(trace_blocks), dim3(kBlock), lds, stream, ta);
+        launch_trace(ta, false, planes_only, trace_blocks, lds, stream);
         HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
         HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
         float m = 0.f;
@@ -1378,6 +1702,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       const unsigned long long cr = cnt[2] - dg[0], cb = cnt[0] - dg[1];
       std::fprintf(stderr, "[rt diag] shadow rays %llu: %.1f box tests/ray; other rays %llu: %.1f box tests/ray\n", dg[0],
                    (double)dg[1] / (double)std::max(dg[0], 1ull), cr, (double)cb / (double)std::max(cr, 1ull));
+      unsigned long long wv[3] = {0, 0, 0};  // lane node visits, wave node visits, wave prim tests (ctl bytes 488..)
+      HIP_TRY(hipMemcpy(wv, ctl + 122, sizeof(wv), hipMemcpyDeviceToHost), RT_EDEVICE);
+      std::fprintf(stderr, "[rt diag] node visits: %.2f/ray, lane utilisation %.3f; prim tests: %.2f/ray, lane utilisation %.3f; wave prim-test iterations per wave node visit %.2f\n",
+                   (double)wv[0] / (double)std::max(cnt[2], 1ull), (double)wv[0] / (64.0 * (double)std::max(wv[1], 1ull)),
+                   (double)cnt[1] / (double)std::max(cnt[2], 1ull), (double)cnt[1] / (64.0 * (double)std::max(wv[2], 1ull)),
+                   (double)wv[2] / (double)std::max(wv[1], 1ull));
     }
   }
   return RT_OK;
