@@ -54,7 +54,10 @@ static int lds_stack_entries() {
 constexpr int kFetchShards = 8;    // trace work counters (one per XCD-sized slice of the slots)
 constexpr int kFetchStride = 32;   // u32 words between counters: one 128-B line each
 constexpr int kCtlBytes = 4096;    // control block; per-step reset region at byte 2048
-constexpr int kBatchShards = 32;  // sharded work counters: no hot atomic word  // traversal stack entries per lane held in LDS (rest spill to HBM)
+// Batch-claim counters of the logic step: one per 128-B line (kCtrStride words apart) --
+// atomics on one line serialise at the memory side, so the shards must not share lines.
+constexpr int kMaxBatchShards = 1024;
+constexpr int kCtrStride = 32;
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
@@ -104,11 +107,14 @@ struct LogicArgs {
   uint64_t seed_key;
   // work
   const int* tile_ids;
+  int tile_affine;            // tile_ids[i] == tile_first + i * tile_step (no table lookup)
+  int tile_first, tile_step;
   int tile_w, tile_h, tiles_x, sub_x;
   int n_pixels;  // n_tiles * tile_w * tile_h (launch-local pixel space)
   int n_samples; // s*s (1 when s <= 1)
   long long n_units;  // n_pixels * n_samples
-  unsigned int* batch_ctr;  // kBatchShards counters; wave w pulls batches from counter w % kBatchShards
+  unsigned int* batch_ctr;  // batch_shards counters, kCtrStride words apart; wave w pulls from w % batch_shards
+  int batch_shards;
   float* samples;  // [n_units][3] per-sample Trace colours
   float* out;
   // buffers
@@ -122,6 +128,7 @@ struct LogicArgs {
   int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
+  unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it)
 };
 
 struct TraceArgs {
@@ -144,6 +151,8 @@ struct TraceArgs {
   int has_tex;                // some material is textured: hit u, v needed
   int refill_min;             // refill kernel: refill finished lanes when fewer than this many traverse
   int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
+  int diag;                   // count_work under RT_DIAG: wave-level utilisation counters
+  const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
 };
 
 // ---------------------------------------------------------------- traversal
@@ -199,7 +208,7 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
     float t;
     if (kCount) {
       ++nprim;
-      if (__lane_id() == __ffsll((long long)__ballot(1)) - 1) atomicAdd(a.counters + 61, 1ull);  // wave-level prim tests
+      if (a.diag && __lane_id() == __ffsll((long long)__ballot(1)) - 1) atomicAdd(a.counters + 61, 1ull);  // wave-level prim tests
     }
     if (!prim_hit<false, kPlanesOnly>(P, rec, r, t, nullptr)) continue;
     const int2 ref = a.prim_refs[pi];
@@ -313,7 +322,7 @@ __device__ __forceinline__ void node_step(const TraceArgs& a, const Query& q, Hi
   }
   if (kCount) {
     const uint64_t wm = __ballot(1);
-    if (__lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
+    if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
     ++nvisit;
     const unsigned nb = __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
                                             (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
@@ -567,7 +576,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, co
   const float tz1[4] = {t_lz01.x, t_lz01.y, t_lz23.x, t_lz23.y}, tz2[4] = {t_hz01.x, t_hz01.y, t_hz23.x, t_hz23.y};
   if (kCount) {
     const uint64_t wm = __ballot(1);
-    if (__lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
+    if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
     ++nvisit;
     const unsigned nb = __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
                                             (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
@@ -667,6 +676,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             if (len > 0 && base < len) {
               q_next = st0 + base;
               q_end = st0 + min(base + 64u, len);
+              // 64-slot groups are slot-waves of the logic step: skip one whose slots retired
+              if (a.wave_done[q_next >> 6] != 0u) continue;
               break;
             }
             if (++sk >= kFetchShards) {
@@ -774,7 +785,7 @@ __device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, 
   const int tl = p / tile_px, r = p - tl * tile_px;
   const int b = r >> 6, l = r & 63;
   const int lx = (b % a.sub_x) * 8 + (l & 7), ly = (b / a.sub_x) * 8 + (l >> 3);
-  const int tid = a.tile_ids[tl];
+  const int tid = a.tile_affine ? a.tile_first + tl * a.tile_step : a.tile_ids[tl];
   x = (tid % a.tiles_x) * a.tile_w + lx;
   y = (tid / a.tiles_x) * a.tile_h + ly;
   out_off = ((size_t)tl * tile_px + (size_t)ly * a.tile_w + lx) * 3;
@@ -784,8 +795,10 @@ __device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, 
 // ---------------------------------------------------------------- logic kernel
 // unit -> (launch-local pixel, sample); false if the pixel lies outside the image
 __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, int& px, int& py, int& sample) {
-  const int p = (int)(unit / a.n_samples);
-  sample = (int)(unit - (long long)p * a.n_samples);
+  // units < 2^31 (checked on the host): 32-bit unsigned division
+  const unsigned u = (unsigned)unit, ns = (unsigned)a.n_samples;
+  const int p = (int)(u / ns);
+  sample = (int)(u - (unsigned)p * ns);
   size_t off;
   return pixel_coords(a, p, px, py, off);
 }
@@ -799,6 +812,8 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
 template <bool kFrames, bool kTex, bool kPlanes>
 __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
+  // a wave whose slots all retired has nothing left in this frame (one scalar load)
+  if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
   bool want = false;
   if (slot < a.n_slots) {
     const int N = a.n_slots;
@@ -894,12 +909,12 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
         // the whole wave finished its batch: pull the next 64 consecutive samples (one pixel's
         // worth -> coherent rays) from this wave's counter shard
         const int wave = (int)(slot >> 6);
-        const int shard = wave % kBatchShards;
+        const int shard = wave % a.batch_shards;
         const int leader = __ffsll((long long)__ballot(1)) - 1;  // lowest active lane
         unsigned int j = 0;
-        if ((threadIdx.x & 63) == leader) j = atomicAdd(a.batch_ctr + shard, 1u);
+        if ((threadIdx.x & 63) == leader) j = atomicAdd(a.batch_ctr + shard * kCtrStride, 1u);
         j = __shfl(j, leader);
-        const long long batch = (long long)j * kBatchShards + shard;
+        const long long batch = (long long)j * a.batch_shards + shard;
         unit = batch * 64 + (threadIdx.x & 63);
         idle = false;
         if (batch * 64 >= a.n_units || unit >= a.n_units) {
@@ -1135,6 +1150,7 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       // pass 2 only when no lane of the wave has a query and the wave is not finished
       if (__ballot(want || (!idle && !retired)) != 0ull || __ballot(!retired) == 0ull) break;
      }
+      if (__ballot(!retired) == 0ull && (threadIdx.x & 63) == 0) a.wave_done[slot >> 6] = 1u;
       if (retired) {
         stu(F_UNIT, 0xFFFFFFFFu);
         a.query[Q_KIND * N + slot] = __int_as_float(-1);
@@ -1237,11 +1253,12 @@ __global__ __launch_bounds__(kBlock) void quantise_kernel(const float* rgb, long
 // slot initialisation: slot k takes unit k (units past the end retire immediately); a unit
 // whose pixel is outside the image (edge tiles) is skipped by the first logic step.
 __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, long long n_units, int* result,
-                                                      float* query) {
+                                                      float* query, unsigned int* wave_done) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
   if (slot >= n_slots) return;
   for (int f = 0; f < F_COUNT; ++f) state[f * n_slots + slot] = 0u;
   state[F_UNIT * n_slots + slot] = (uint32_t)-2;  // idle: the first logic step pulls a batch
+  if ((slot & 63) == 0) wave_done[slot >> 6] = 0u;
   state[F_CTRL * n_slots + slot] = ST_SAMPLE;
   result[slot] = -1;
   query[Q_KIND * n_slots + slot] = __int_as_float(-1);
@@ -1271,6 +1288,13 @@ void launch_trace(const TraceArgs& ta, bool count, bool planes, unsigned blocks,
       else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
     }
   }
+}
+static int batch_shards_env() {
+  static const int v = [] {
+    const char* e = std::getenv("RT_BATCH_SHARDS");
+    return e ? std::max(1, std::min(kMaxBatchShards, std::atoi(e))) : 32;
+  }();
+  return v;
 }
 static int leaf_min_env() {
   static const int v = [] {
@@ -1336,7 +1360,7 @@ struct rt_scene_s {
   size_t spill_cap = 0;
   // per-render workspace (grown on demand)
   void* d_ctl = nullptr;  // bytes 16/24: box/prim tests, 32: rays (u64), 2048: trace work counters, 3072: any_query,
-                          // 256: batch counter shards (kBatchShards x u32)
+                          // batch-claim counters: d_batch_ctr
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
   uint32_t* d_state = nullptr;
@@ -1347,15 +1371,18 @@ struct rt_scene_s {
   size_t samples_cap = 0;
   int* d_result = nullptr;
   float* d_hit = nullptr;
+  unsigned int* d_wave_done = nullptr;
   size_t slots_cap = 0;
   unsigned int* h_flag = nullptr;  // pinned
+  unsigned int* d_batch_ctr = nullptr;  // kMaxBatchShards counters, one 128-B line each
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_a = nullptr, ev_b = nullptr;
 };
 
 static void free_workspace(rt_scene_s* s) {
-  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples, s->d_hit};
+  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples, s->d_hit, s->d_wave_done};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  s->d_wave_done = nullptr;
   s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
   s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr; s->d_hit = nullptr;
   s->slots_cap = 0;
@@ -1397,7 +1424,7 @@ int rt_scene_destroy(rt_scene_t s) {
   (void)hipDeviceSynchronize();
   free_workspace(s);
   void* ptrs[] = {s->d_prims, s->d_nodes, s->d_mats, s->d_lights, s->d_tex, s->d_texels, s->d_ctl, s->d_tiles,
-                  s->d_prim_refs, s->d_ref_boxes, s->d_spill};
+                  s->d_prim_refs, s->d_ref_boxes, s->d_spill, s->d_batch_ctr};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
@@ -1454,6 +1481,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     return rc;
   }
   if (hipMalloc(&s->d_ctl, kCtlBytes) != hipSuccess || hipHostMalloc((void**)&s->h_flag, 64) != hipSuccess ||
+      hipMalloc(&s->d_batch_ctr, (size_t)kMaxBatchShards * kCtrStride * 4) != hipSuccess ||
       hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
       hipEventCreate(&s->ev_a) != hipSuccess || hipEventCreate(&s->ev_b) != hipSuccess) {
     rt_scene_destroy(s);
@@ -1470,6 +1498,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     const size_t lds_bytes = (size_t)lds_entries * kBlock * (refill ? 2 * sizeof(int) : sizeof(int));
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kBlock, lds_bytes) != hipSuccess || bpc < 1)
       bpc = 2;
+    if (const char* e = std::getenv("RT_TRACE_BPC")) bpc = std::max(1, std::min(bpc, std::atoi(e)));  // diagnostic
     s->n_cu = ncu;
     s->trace_blocks_per_cu = bpc;
   }
@@ -1506,6 +1535,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const bool planes_only = s->desc.prim_stride == 64;
   const int n_samples = p->spp_sqrt <= 1 ? 1 : p->spp_sqrt * p->spp_sqrt;
   const long long n_units = (long long)n_pixels * n_samples;
+  if (n_units > 0x7ffffff0LL) return fail(RT_EINVAL, "rt_render_tiles: too many samples in one call (split the tiles)");
   // whole blocks of slots; a wave renders 64 consecutive samples per batch
   // Slots in flight, sized to this call's samples (measured, 1024^2 x 100 spp soup): the whole
   // frame (105M samples) runs best with 16M, one rank's share of a 2-way split (52M) with 13M,
@@ -1529,6 +1559,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_hit, N * HIT_COUNT * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_wave_done, (N / 64 + 1) * 4), RT_ENOMEM);
     if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
     if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
     s->slots_cap = N;
@@ -1563,6 +1594,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.light_samples = p->light_samples;
   la.seed_key = mix64_host(p->seed + 0x9E3779B97F4A7C15ull);
   la.tile_ids = s->d_tiles;
+  // affine tile lists (one GPU: 0, 1, 2 ...; round-robin ranks: r, r + N ...) need no lookup
+  la.tile_first = tile_ids[0];
+  la.tile_step = n_tiles > 1 ? tile_ids[1] - tile_ids[0] : 1;
+  la.tile_affine = 1;
+  for (int i = 0; i < n_tiles && la.tile_affine; ++i) la.tile_affine = tile_ids[i] == la.tile_first + i * la.tile_step;
   la.tile_w = tile_w;
   la.tile_h = tile_h;
   la.tiles_x = tiles_x;
@@ -1582,7 +1618,10 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.late_draws = s->late_draws ? 1 : 0;
   la.pinhole = cam->aperture <= 0.0f ? 1 : 0;
   la.any_query = ctl + 768;  // byte 3072
-  la.batch_ctr = ctl + 64;  // byte 256
+  la.wave_done = s->d_wave_done;
+  la.batch_ctr = s->d_batch_ctr;
+  la.batch_shards = batch_shards_env();
+  HIP_TRY(hipMemsetAsync(s->d_batch_ctr, 0, (size_t)la.batch_shards * kCtrStride * 4, stream), RT_EDEVICE);
 
   TraceArgs ta{};
   ta.c = c;
@@ -1596,12 +1635,14 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   ta.fetch = ctl + 512;  // byte 2048: kFetchShards counters, 128 B apart
   ta.any_query = ctl + 768;
+  ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries());
   // the refill kernel's leaf items hold first << 7 in 31 bits
   ta.refill_min = s->desc.n_prims < (1 << 24) ? refill_min_env() : 0;
   ta.leaf_min = leaf_min_env();
+  ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
   const unsigned trace_blocks = (unsigned)std::max(1, std::min(s->n_cu * s->trace_blocks_per_cu,
                                                                (n_slots + kBlock - 1) / kBlock));
   ta.n_threads = (int)trace_blocks * kBlock;
@@ -1620,7 +1661,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result,
-                     s->d_query);
+                     s->d_query, s->d_wave_done);
   HIP_TRY(hipGetLastError(), RT_EDEVICE);
 
   // ---- iterate logic -> trace until no slot issues a query
