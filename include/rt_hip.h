@@ -73,8 +73,10 @@ typedef struct rt_prim {
  * as the plain (lo - o) * inv form, far inside the boxes' 1e-5 * scale padding.
  *   exps: e_x | e_y << 8 | e_z << 16 (biased binary32 exponents of the grid steps)
  *   q_lo_x: byte k = child k's lo.x code (likewise q_hi_x .. q_hi_z)
- *   meta byte k: 0 = no child; 0x01 = internal child (child[k] = node index);
- *                0x80 | n = leaf child with n primitives starting at child[k]. */
+ *   meta byte k: 0 = no child (child[k] = -1, codes lo 255 / hi 0: an inverted box);
+ *                0x01 = internal child (child[k] = node index);
+ *                0x80 | n = leaf child with n primitives starting at f:
+ *                child[k] = 0x80000000 | f << 7 | n  (f < 2^24, n < 128). */
 typedef struct rt_node4 {
   float origin[3];
   uint32_t exps;

@@ -51,8 +51,8 @@ static int lds_stack_entries() {
   }();
   return v;
 }
-constexpr int kFetchShards = 8;    // trace work counters (one per XCD-sized slice of the slots)
-constexpr int kFetchStride = 32;   // u32 words between counters: one 128-B line each
+constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
+constexpr int kFetchStride = 32;      // u32 words between counters
 constexpr int kCtlBytes = 4096;    // control block; per-step reset region at byte 2048
 // Batch-claim counters of the logic step: one per 128-B line (kCtrStride words apart) --
 // atomics on one line serialise at the memory side, so the shards must not share lines.
@@ -139,7 +139,8 @@ struct TraceArgs {
   int n_nodes;
   const float* query;
   int* result;
-  unsigned int* fetch;        // kFetchShards work counters over slot slices (zeroed per step)
+  unsigned int* fetch;        // fetch_shards work counters over slot slices (zeroed per step)
+  int fetch_shards;
   const unsigned int* any_query;  // logic's "some slot has a query" flag for this step
   unsigned long long* rays;   // queries traced (one atomic per wave at exit)
   int n_slots;
@@ -248,6 +249,7 @@ struct Query {
   float tmax;   // shadow: light distance
   bool any;     // shadow query: any hit with t <= tmax
   uint32_t par; // bit i: fabs(d_i) < 1e-6 (double), the exact slab's parallel test
+  uint32_t sgn; // bit i: inv_i < 0 (the near planes along axis i are the boxes' hi)
 };
 
 // Reads slot's query record; false if the slot emitted no query this step.
@@ -271,6 +273,7 @@ __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query&
     return 1.0f / dd;
   };
   q.inv = V3{safe_inv(q.r.d.x), safe_inv(q.r.d.y), safe_inv(q.r.d.z)};
+  q.sgn = (q.inv.x < 0.0f ? 1u : 0u) | (q.inv.y < 0.0f ? 2u : 0u) | (q.inv.z < 0.0f ? 4u : 0u);
   return true;
 }
 
@@ -343,7 +346,7 @@ __device__ __forceinline__ void node_step(const TraceArgs& a, const Query& q, Hi
     const int k = __builtin_ctz(leaves);
     leaves &= leaves - 1u;
     const float tk = k == 0 ? tn[0] : k == 1 ? tn[1] : k == 2 ? tn[2] : tn[3];
-    const int ck = k == 0 ? cc[0] : k == 1 ? cc[1] : k == 2 ? cc[2] : cc[3];
+    const int ck = (int)(((uint32_t)(k == 0 ? cc[0] : k == 1 ? cc[1] : k == 2 ? cc[2] : cc[3]) & 0x7fffffffu) >> 7);
     float lim = any ? tmax : h.best_t;
     lim = lim + (lim * 1e-5f + a.c.eps_abs);
     if (!(tk > lim))
@@ -462,12 +465,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
   unsigned long long dg_any_rays = 0, dg_any_box = 0;  // kCount diagnostics: shadow (any-hit) queries
   const TraceArgs& a = ta;
   if (*ta.any_query == 0u) return;  // no slot emitted a query this step
-  // The slots are cut into kFetchShards slices with a counter each (one device-wide counter
+  // The slots are cut into fetch_shards slices with a counter each (one device-wide counter
   // serialises at ~12 ns per 64-slot fetch: 1.6 ms per 8M-slot launch); a wave drains the
   // slice of its block (blockIdx % 8 ~ its XCD) first, then helps the others.
-  const unsigned shard_len = (((nq + kFetchShards - 1) / kFetchShards) + 63u) & ~63u;
-  for (int sk = 0; sk < kFetchShards; ++sk) {
-   const int sh = (int)((blockIdx.x + sk) % kFetchShards);
+  const unsigned nfs = (unsigned)ta.fetch_shards;
+  const unsigned shard_len = (((nq + nfs - 1) / nfs) + 63u) & ~63u;
+  for (int sk = 0; sk < (int)nfs; ++sk) {
+   const int sh = (int)((blockIdx.x + sk) % nfs);
    const unsigned sh_start = (unsigned)sh * shard_len;
    if (sh_start >= nq) continue;
    const unsigned sh_len = min(shard_len, nq - sh_start);
@@ -545,8 +549,14 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // One 4-wide node visit: every child box the ray enters within the bound -- internal nodes
 // and leaves alike -- is ordered by t_near; the three farthest are pushed, the nearest
 // becomes the lane's item (a leaf item waits for the next leaf phase).
+//
+// Per axis the ray's direction sign picks which of the two code words holds the near planes
+// of all four children (inv > 0: lo, else hi), so each child needs one max3 and one min3
+// instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
+// always miss; child entries come precomputed from the host (node index, or the encoded
+// leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
 template <bool kCount>
-__device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, const HitState& h, int node,
+__device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, float lim, int node,
                                           const LaneStack& S, int& sp, int gtid, unsigned int& nbox,
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
@@ -557,24 +567,27 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, co
   const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
   const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
   const uint32_t ex = __float_as_uint(g.w);
-  const uint32_t meta = qb.z;
   const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
   const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
   const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
   const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
+  const uint32_t nxw = (q.sgn & 1u) ? qa.y : qa.x, fxw = (q.sgn & 1u) ? qa.x : qa.y;
+  const uint32_t nyw = (q.sgn & 2u) ? qa.w : qa.z, fyw = (q.sgn & 2u) ? qa.z : qa.w;
+  const uint32_t nzw = (q.sgn & 4u) ? qb.y : qb.x, fzw = (q.sgn & 4u) ? qb.x : qb.y;
   const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
   auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
   auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };
-  const f32x2 t_lx01 = __builtin_elementwise_fma(lo2(qa.x), Bx, Ax), t_lx23 = __builtin_elementwise_fma(hi2(qa.x), Bx, Ax);
-  const f32x2 t_hx01 = __builtin_elementwise_fma(lo2(qa.y), Bx, Ax), t_hx23 = __builtin_elementwise_fma(hi2(qa.y), Bx, Ax);
-  const f32x2 t_ly01 = __builtin_elementwise_fma(lo2(qa.z), By, Ay), t_ly23 = __builtin_elementwise_fma(hi2(qa.z), By, Ay);
-  const f32x2 t_hy01 = __builtin_elementwise_fma(lo2(qa.w), By, Ay), t_hy23 = __builtin_elementwise_fma(hi2(qa.w), By, Ay);
-  const f32x2 t_lz01 = __builtin_elementwise_fma(lo2(qb.x), Bz, Az), t_lz23 = __builtin_elementwise_fma(hi2(qb.x), Bz, Az);
-  const f32x2 t_hz01 = __builtin_elementwise_fma(lo2(qb.y), Bz, Az), t_hz23 = __builtin_elementwise_fma(hi2(qb.y), Bz, Az);
-  const float tx1[4] = {t_lx01.x, t_lx01.y, t_lx23.x, t_lx23.y}, tx2[4] = {t_hx01.x, t_hx01.y, t_hx23.x, t_hx23.y};
-  const float ty1[4] = {t_ly01.x, t_ly01.y, t_ly23.x, t_ly23.y}, ty2[4] = {t_hy01.x, t_hy01.y, t_hy23.x, t_hy23.y};
-  const float tz1[4] = {t_lz01.x, t_lz01.y, t_lz23.x, t_lz23.y}, tz2[4] = {t_hz01.x, t_hz01.y, t_hz23.x, t_hz23.y};
+  const f32x2 nx01 = __builtin_elementwise_fma(lo2(nxw), Bx, Ax), nx23 = __builtin_elementwise_fma(hi2(nxw), Bx, Ax);
+  const f32x2 fx01 = __builtin_elementwise_fma(lo2(fxw), Bx, Ax), fx23 = __builtin_elementwise_fma(hi2(fxw), Bx, Ax);
+  const f32x2 ny01 = __builtin_elementwise_fma(lo2(nyw), By, Ay), ny23 = __builtin_elementwise_fma(hi2(nyw), By, Ay);
+  const f32x2 fy01 = __builtin_elementwise_fma(lo2(fyw), By, Ay), fy23 = __builtin_elementwise_fma(hi2(fyw), By, Ay);
+  const f32x2 nz01 = __builtin_elementwise_fma(lo2(nzw), Bz, Az), nz23 = __builtin_elementwise_fma(hi2(nzw), Bz, Az);
+  const f32x2 fz01 = __builtin_elementwise_fma(lo2(fzw), Bz, Az), fz23 = __builtin_elementwise_fma(hi2(fzw), Bz, Az);
+  const float tnx[4] = {nx01.x, nx01.y, nx23.x, nx23.y}, tfx[4] = {fx01.x, fx01.y, fx23.x, fx23.y};
+  const float tny[4] = {ny01.x, ny01.y, ny23.x, ny23.y}, tfy[4] = {fy01.x, fy01.y, fy23.x, fy23.y};
+  const float tnz[4] = {nz01.x, nz01.y, nz23.x, nz23.y}, tfz[4] = {fz01.x, fz01.y, fz23.x, fz23.y};
   if (kCount) {
+    const uint32_t meta = qb.z;
     const uint64_t wm = __ballot(1);
     if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
     ++nvisit;
@@ -583,41 +596,39 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, co
     nbox += nb;
     if (q.any) dg_any_box += nb;
   }
-  const float lim = cull_limit(a, q, h);
+  // entered within the bound: max(t_near, 0) <= min(t_far, lim)  (lim > 0 always), i.e.
+  // t_near <= t_far, t_far >= 0 and t_near <= lim; misses sort last as (inf, entry)
   float t[4];
   int c[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float n0 = fmaxf(fmaxf(fminf(tx1[k], tx2[k]), fminf(ty1[k], ty2[k])), fminf(tz1[k], tz2[k]));
-    const float f0 = fminf(fminf(fmaxf(tx1[k], tx2[k]), fmaxf(ty1[k], ty2[k])), fmaxf(tz1[k], tz2[k]));
-    const uint32_t m = (meta >> (8 * k)) & 0xffu;
-    const bool hit = m != 0u && n0 <= f0 && f0 >= 0.0f && !(n0 > lim);
-    const int e = (m & 0x80u) ? (int)(kLeafBit | ((uint32_t)cc[k] << 7) | (m & 0x7fu)) : cc[k];
-    t[k] = hit ? n0 : __builtin_inff();
-    c[k] = hit ? e : kNoItem;
+    const float n0 = fmaxf(fmaxf(tnx[k], tny[k]), fmaxf(tnz[k], 0.0f));
+    const float f0 = fminf(fminf(tfx[k], tfy[k]), fminf(tfz[k], lim));
+    t[k] = n0 <= f0 ? n0 : __builtin_inff();
+    c[k] = cc[k];
   }
-  // sort 4 (t, entry) ascending; misses (kNoItem, inf) sink to the end
+  // sort 4 (t, entry) ascending
   cswap(t[0], c[0], t[1], c[1]);
   cswap(t[2], c[2], t[3], c[3]);
   cswap(t[0], c[0], t[2], c[2]);
   cswap(t[1], c[1], t[3], c[3]);
   cswap(t[1], c[1], t[2], c[2]);
-  // push the three farther children far-to-near.  The valid entries are a prefix of the
-  // sorted four, so unconditional writes at sp, sp+v3, sp+v3+v2 leave exactly the valid ones
-  // below the new top (an invalid one lands on the top slot and is overwritten or abandoned).
+  const bool v3 = t[3] != __builtin_inff(), v2 = t[2] != __builtin_inff(), v1 = t[1] != __builtin_inff();
+  // push the three farther children far-to-near.  The entries entered are a prefix of the
+  // sorted four, so unconditional writes at sp, sp+v3, sp+v3+v2 leave exactly those below
+  // the new top (a missed one lands on the top slot and is overwritten or abandoned).
   if (__ballot(sp + 3 > a.lds_entries) == 0ull) {
-    const int v3 = c[3] != kNoItem, v2 = c[2] != kNoItem, v1 = c[1] != kNoItem;
     int2* st = S.e + sp * kBlock;
     st[0] = make_int2(c[3], __float_as_int(t[3]));
-    st[v3 * kBlock] = make_int2(c[2], __float_as_int(t[2]));
-    st[(v3 + v2) * kBlock] = make_int2(c[1], __float_as_int(t[1]));
-    sp += v3 + v2 + v1;
+    st[(int)v3 * kBlock] = make_int2(c[2], __float_as_int(t[2]));
+    st[((int)v3 + (int)v2) * kBlock] = make_int2(c[1], __float_as_int(t[1]));
+    sp += (int)v3 + (int)v2 + (int)v1;
   } else {
-    if (c[3] != kNoItem) stack_push(a, S, sp, gtid, c[3], t[3]);
-    if (c[2] != kNoItem) stack_push(a, S, sp, gtid, c[2], t[2]);
-    if (c[1] != kNoItem) stack_push(a, S, sp, gtid, c[1], t[1]);
+    if (v3) stack_push(a, S, sp, gtid, c[3], t[3]);
+    if (v2) stack_push(a, S, sp, gtid, c[2], t[2]);
+    if (v1) stack_push(a, S, sp, gtid, c[1], t[1]);
   }
-  if (c[0] != kNoItem) return c[0];
+  if (t[0] != __builtin_inff()) return c[0];
   return stack_pop_live(a, S, sp, gtid, lim);
 }
 
@@ -641,7 +652,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
   unsigned long long dg_any_rays = 0, dg_any_box = 0;
   const TraceArgs& a = ta;
   if (*ta.any_query == 0u) return;
-  const unsigned shard_len = (((nq + kFetchShards - 1) / kFetchShards) + 63u) & ~63u;
+  const unsigned nfs = (unsigned)ta.fetch_shards;
+  const unsigned shard_len = (((nq + nfs - 1) / nfs) + 63u) & ~63u;
   // wave-uniform work queue: [q_next, q_end)
   int sk = 0;
   unsigned q_next = 0, q_end = 0;
@@ -649,6 +661,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
   // lane state
   int slot = -1;        // query owned by this lane (traversing, or finished awaiting write-back)
   int item = kNoItem;   // node to visit / leaf to test next; kNoItem: traversal finished
+  float lim = 0.0f;     // cull bound of the query (cull_limit), refreshed after each leaf test
   Query q;
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
   int sp = 0;
@@ -665,7 +678,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         if (freem == 0ull) break;
         if (q_next >= q_end) {  // next 64 slots: this shard's counter, then the other shards'
           for (;;) {
-            const int sh = (int)((blockIdx.x + sk) % kFetchShards);
+            const int sh = (int)((blockIdx.x + sk) % nfs);
             const unsigned st0 = (unsigned)sh * shard_len;
             const unsigned len = st0 < nq ? min(shard_len, nq - st0) : 0u;
             unsigned base = 0;
@@ -680,7 +693,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
               if (a.wave_done[q_next >> 6] != 0u) continue;
               break;
             }
-            if (++sk >= kFetchShards) {
+            if (++sk >= (int)nfs) {
               exhausted = true;
               break;
             }
@@ -696,6 +709,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
             ++nrays;
             if (kCount && q.any) ++dg_any_rays;
             h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
+            lim = cull_limit(a, q, h);
             sp = 0;
             item = (a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem;
             if (a.c.n_prims > 0 && !a.c.use_bvh)  // BVH::intersect_linear (acceleration.cpp:124-139)
@@ -718,11 +732,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) 
         const uint32_t e = (uint32_t)item;
         test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
                                         true, h, nprim);
-        item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, cull_limit(a, q, h));
+        lim = cull_limit(a, q, h);
+        item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
       }
     }
     // node phase
-    if (item >= 0) item = node_visit<kCount>(a, q, h, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
   }
   trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
 }
@@ -1289,6 +1304,13 @@ void launch_trace(const TraceArgs& ta, bool count, bool planes, unsigned blocks,
     }
   }
 }
+static int fetch_shards_env() {
+  static const int v = [] {
+    const char* e = std::getenv("RT_FETCH_SHARDS");
+    return e ? std::max(1, std::min(kMaxFetchShards, std::atoi(e))) : 8;
+  }();
+  return v;
+}
 static int batch_shards_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_BATCH_SHARDS");
@@ -1375,6 +1397,7 @@ struct rt_scene_s {
   size_t slots_cap = 0;
   unsigned int* h_flag = nullptr;  // pinned
   unsigned int* d_batch_ctr = nullptr;  // kMaxBatchShards counters, one 128-B line each
+  unsigned int* d_fetch = nullptr;      // trace fetch counters (one line each) + any_query line
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_a = nullptr, ev_b = nullptr;
 };
 
@@ -1424,7 +1447,7 @@ int rt_scene_destroy(rt_scene_t s) {
   (void)hipDeviceSynchronize();
   free_workspace(s);
   void* ptrs[] = {s->d_prims, s->d_nodes, s->d_mats, s->d_lights, s->d_tex, s->d_texels, s->d_ctl, s->d_tiles,
-                  s->d_prim_refs, s->d_ref_boxes, s->d_spill, s->d_batch_ctr};
+                  s->d_prim_refs, s->d_ref_boxes, s->d_spill, s->d_batch_ctr, s->d_fetch};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
@@ -1437,10 +1460,10 @@ int rt_scene_destroy(rt_scene_t s) {
 
 int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   if (!d || !out) return fail(RT_EINVAL, "rt_scene_create: null argument");
-  if (d->n_prims < 0 || (d->n_prims > 0 && (!d->prims || !d->prim_refs)) ||
+  if (d->n_prims < 0 || d->n_prims >= (1 << 24) || (d->n_prims > 0 && (!d->prims || !d->prim_refs)) ||
       (d->n_prims > d->n_unbounded && (d->n_nodes <= 0 || !d->nodes)) || d->n_unbounded < 0 ||
       d->n_unbounded > d->n_prims || (d->n_prims > 0 && (d->n_ref_leaves <= 0 || !d->ref_leaf_boxes)))
-    return fail(RT_EINVAL, "rt_scene_create: inconsistent primitive/node arrays");
+    return fail(RT_EINVAL, "rt_scene_create: inconsistent primitive/node arrays (at most 2^24 - 1 primitives)");
   if (d->stack_bound < 1 || d->stack_bound > 4096) return fail(RT_EINVAL, "rt_scene_create: stack_bound out of range");
   if (d->prim_stride != 64 && d->prim_stride != 128)
     return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
@@ -1454,8 +1477,12 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     for (int k = 0; k < 4; ++k) {
       const uint32_t m = (nd.meta >> (8 * k)) & 0xffu;
       const int64_t c = nd.child[k];
-      const bool ok = m == 0 || (m == 0x01u && c > i && c < d->n_nodes) ||
-                      ((m & 0x80u) && (m & 0x7fu) != 0 && c >= 0 && c + (m & 0x7fu) <= n_bounded);
+      // leaf entries: 0x80000000 | first << 7 | count (first < 2^24), count == the meta byte's
+      const uint32_t cu = (uint32_t)nd.child[k];
+      const int64_t first = (int64_t)((cu & 0x7fffffffu) >> 7);
+      const bool ok = (m == 0 && nd.child[k] == -1) || (m == 0x01u && c > i && c < d->n_nodes) ||
+                      ((m & 0x80u) && (m & 0x7fu) != 0 && (cu & 0x80000000u) && (cu & 0x7fu) == (m & 0x7fu) &&
+                       first + (m & 0x7fu) <= n_bounded);
       if (!ok) return fail(RT_EINVAL, "rt_scene_create: node child out of range");
     }
   }
@@ -1482,6 +1509,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   }
   if (hipMalloc(&s->d_ctl, kCtlBytes) != hipSuccess || hipHostMalloc((void**)&s->h_flag, 64) != hipSuccess ||
       hipMalloc(&s->d_batch_ctr, (size_t)kMaxBatchShards * kCtrStride * 4) != hipSuccess ||
+      hipMalloc(&s->d_fetch, ((size_t)kMaxFetchShards + 1) * kFetchStride * 4) != hipSuccess ||
       hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
       hipEventCreate(&s->ev_a) != hipSuccess || hipEventCreate(&s->ev_b) != hipSuccess) {
     rt_scene_destroy(s);
@@ -1491,7 +1519,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const int lds_entries = std::min(d->stack_bound, lds_stack_entries());
-    const bool refill = d->n_prims < (1 << 24) && refill_min_env() > 0;
+    const bool refill = refill_min_env() > 0;
     const bool planes = d->prim_stride == 64;
     const void* fn = refill ? (planes ? (const void*)trace_refill_kernel<false, true> : (const void*)trace_refill_kernel<false, false>)
                             : (planes ? (const void*)trace_kernel<false, true> : (const void*)trace_kernel<false, false>);
@@ -1617,7 +1645,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.hit = s->d_hit;
   la.late_draws = s->late_draws ? 1 : 0;
   la.pinhole = cam->aperture <= 0.0f ? 1 : 0;
-  la.any_query = ctl + 768;  // byte 3072
+  la.any_query = s->d_fetch + (size_t)fetch_shards_env() * kFetchStride;  // the line after the fetch counters
   la.wave_done = s->d_wave_done;
   la.batch_ctr = s->d_batch_ctr;
   la.batch_shards = batch_shards_env();
@@ -1633,14 +1661,15 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.result = s->d_result;
   ta.hit = s->d_hit;
   ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
-  ta.fetch = ctl + 512;  // byte 2048: kFetchShards counters, 128 B apart
-  ta.any_query = ctl + 768;
+  ta.fetch = s->d_fetch;
+  ta.fetch_shards = fetch_shards_env();
+  ta.any_query = la.any_query;
   ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries());
   // the refill kernel's leaf items hold first << 7 in 31 bits
-  ta.refill_min = s->desc.n_prims < (1 << 24) ? refill_min_env() : 0;
+  ta.refill_min = refill_min_env();
   ta.leaf_min = leaf_min_env();
   ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
   const unsigned trace_blocks = (unsigned)std::max(1, std::min(s->n_cu * s->trace_blocks_per_cu,
@@ -1674,10 +1703,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
   for (;;) {
     // per-step reset: trace work counters (byte 2048) + any_query (byte 3072)
-    HIP_TRY(hipMemsetAsync(ctl + 512, 0, kFetchShards * kFetchStride * 4 + 4, stream), RT_EDEVICE);
+    // per-step reset: trace work counters + any_query (the line after them)
+    HIP_TRY(hipMemsetAsync(s->d_fetch, 0, ((size_t)ta.fetch_shards + 1) * kFetchStride * 4, stream), RT_EDEVICE);
     launch_logic(la, need_frames, (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0, planes_only, slot_blocks, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipMemcpyAsync(s->h_flag, ctl + 768, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipMemcpyAsync(s->h_flag, la.any_query, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
     launch_trace(ta, p->count_work != 0, planes_only, trace_blocks, lds, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
@@ -1692,7 +1722,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       unsigned long long rays0 = 0;
       HIP_TRY(hipMemcpy(&rays0, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
       for (int k = 0; k < replay_reps; ++k) {
-        HIP_TRY(hipMemsetAsync(ctl + 512, 0, kFetchShards * kFetchStride * 4, stream), RT_EDEVICE);
+        HIP_TRY(hipMemsetAsync(s->d_fetch, 0, (size_t)ta.fetch_shards * kFetchStride * 4, stream), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
         launch_trace(ta, false, planes_only, trace_blocks, lds, stream);
         HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);

@@ -381,7 +381,8 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
         const Node2& c = B.nodes[kids[k]];
         cb[nk++] = c.box;
         if (c.left < 0) {
-          out.child[k] = c.start;  // first primitive (new order == bounded order)
+          // leaf entry: 0x80000000 | first primitive << 7 | count (new order == bounded order)
+          out.child[k] = (int32_t)(0x80000000u | ((uint32_t)c.start << 7) | (uint32_t)c.count);
           meta |= (0x80u | (uint32_t)c.count) << (8 * k);
         } else {
           out.child[k] = emit(kids[k], it.depth + 1);

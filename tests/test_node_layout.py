@@ -67,7 +67,10 @@ def check_tree(sc):
                 stack.append((c, boxes + [box]))
             else:
                 n = m & 0x7F
-                assert m & 0x80 and n >= 1 and 0 <= c and c + n <= n_bounded
+                cu = c & 0xFFFFFFFF  # leaf entry: 0x80000000 | first << 7 | n
+                assert m & 0x80 and n >= 1 and cu & 0x80000000 and (cu & 0x7F) == n
+                c = (cu & 0x7FFFFFFF) >> 7
+                assert c + n <= n_bounded
                 covered[c:c + n] += 1
                 for p in range(c, c + n):
                     if not is_plane[p]:
