@@ -213,7 +213,8 @@ __device__ __forceinline__ bool in_tri(V3 P, V3 A, V3 B, V3 C, V3 n) {
 // ---- Plane::intersect (shapes.cpp:444-494); normal precomputed on the host with the
 // identical ops (the reference recomputes it per call, same bits).
 template <bool kAttr>
-__device__ __forceinline__ bool plane_hit(const PrimA& P, const Ray& ray, float& t_out, HitAttr* at) {
+__device__ __forceinline__ bool plane_hit(const PrimA& P, const Ray& ray, float& t_out, HitAttr* at,
+                                          V3* x_out = nullptr) {
   if (!(prim_tag(P) & RT_TAG_PLANE_VALID)) return false;
   V3 c0{P.a[0], P.a[1], P.a[2]}, c1{P.a[4], P.a[5], P.a[6]}, c2{P.a[8], P.a[9], P.a[10]};
   V3 c3{P.a[12], P.a[13], P.a[14]};
@@ -225,6 +226,7 @@ __device__ __forceinline__ bool plane_hit(const PrimA& P, const Ray& ray, float&
   V3 X{ray.o.x + t * ray.d.x, ray.o.y + t * ray.d.y, ray.o.z + t * ray.d.z};
   if (!in_tri(X, c1, c3, c2, n) && !in_tri(X, c0, c1, c2, n)) return false;
   t_out = t;
+  if (x_out) *x_out = X;
   if (kAttr) {
     V3 vu = sub(c1, c0), vv = sub(c3, c0), hv = sub(X, c0);
     float u = ((dot(hv, vu)) / (dot(vu, vu)));

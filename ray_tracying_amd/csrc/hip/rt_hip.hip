@@ -164,6 +164,10 @@ struct HitState {
   int best_ref;   // reference index of the best hit (tie-break, acceleration.cpp:112)
   int best_idx;   // primitive index (traversal order) of the best hit, -1 = miss
   bool done;      // any-hit: occluded
+  // planes-only scenes: the best hit's record, kept when it is found (Plane::intersect's hit
+  // point and the precomputed normal, shapes.cpp:472-480) so the write-back needs no re-test
+  V3 p, n;
+  uint32_t mat;
 };
 
 // The reference accepts a primitive's hit only if its reference leaf box passes the exact
@@ -211,7 +215,12 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
       ++nprim;
       if (a.diag && __lane_id() == __ffsll((long long)__ballot(1)) - 1) atomicAdd(a.counters + 61, 1ull);  // wave-level prim tests
     }
-    if (!prim_hit<false, kPlanesOnly>(P, rec, r, t, nullptr)) continue;
+    V3 X;
+    if (kPlanesOnly) {
+      if (!plane_hit<false>(P, r, t, nullptr, &X)) continue;
+    } else if (!prim_hit<false, false>(P, rec, r, t, nullptr)) {
+      continue;
+    }
     const int2 ref = a.prim_refs[pi];
     auto leaf_ok = [&]() {
       if (!check_leaf || ref.y < 0) return true;
@@ -228,6 +237,11 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
       h.best_t = t;
       h.best_ref = ref.x;
       h.best_idx = pi;
+      if (kPlanesOnly) {
+        h.p = X;
+        h.n = V3{P.a[3], P.a[7], P.a[11]};
+        h.mat = RT_TAG_MATERIAL(prim_tag(P));
+      }
     }
   }
 }
@@ -249,7 +263,8 @@ struct Query {
   float tmax;   // shadow: light distance
   bool any;     // shadow query: any hit with t <= tmax
   uint32_t par; // bit i: fabs(d_i) < 1e-6 (double), the exact slab's parallel test
-  uint32_t sgn; // bit i: inv_i < 0 (the near planes along axis i are the boxes' hi)
+  uint32_t sel[3];  // per axis, v_perm_b32 selector of the near-plane code word: 0x03020100
+                    // picks the lo word (inv_i >= 0), 0x07060504 the hi word
 };
 
 // Reads slot's query record; false if the slot emitted no query this step.
@@ -268,12 +283,16 @@ __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query&
   par |= ((double)fabsf(q.r.d.y) < 1e-6) ? 2u : 0u;
   par |= ((double)fabsf(q.r.d.z) < 1e-6) ? 4u : 0u;
   q.par = par;
+  // culling only: v_rcp_f32 (1 ulp) instead of a correctly rounded division -- a relative
+  // 2^-23 error in t is far inside the boxes' 1e-5 * scale padding and the pruning margin
   auto safe_inv = [](float d) {
     float dd = fabsf(d) < 1e-12f ? copysignf(1e-12f, d) : d;
-    return 1.0f / dd;
+    return __builtin_amdgcn_rcpf(dd);
   };
   q.inv = V3{safe_inv(q.r.d.x), safe_inv(q.r.d.y), safe_inv(q.r.d.z)};
-  q.sgn = (q.inv.x < 0.0f ? 1u : 0u) | (q.inv.y < 0.0f ? 2u : 0u) | (q.inv.z < 0.0f ? 4u : 0u);
+  q.sel[0] = q.inv.x < 0.0f ? 0x07060504u : 0x03020100u;
+  q.sel[1] = q.inv.y < 0.0f ? 0x07060504u : 0x03020100u;
+  q.sel[2] = q.inv.z < 0.0f ? 0x07060504u : 0x03020100u;
   return true;
 }
 
@@ -400,7 +419,13 @@ __device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const
   if (a.c.use_bvh && !h.done && a.n_unbounded > 0)
     test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, q.any, q.tmax, q.par, true, h, nprim);
   a.result[slot] = q.any ? (h.done ? 1 : 0) : h.best_idx;
-  if (!q.any && h.best_idx >= 0) {
+  if (kPlanesOnly && !a.has_tex && !q.any && h.best_idx >= 0) {
+    // the record captured when the hit was found (no uv without textures)
+    float* H = a.hit;
+    H[(HIT_P + 0) * N + slot] = h.p.x; H[(HIT_P + 1) * N + slot] = h.p.y; H[(HIT_P + 2) * N + slot] = h.p.z;
+    H[(HIT_N + 0) * N + slot] = h.n.x; H[(HIT_N + 1) * N + slot] = h.n.y; H[(HIT_N + 2) * N + slot] = h.n.z;
+    H[HIT_MAT * N + slot] = __uint_as_float(h.mat);
+  } else if (!q.any && h.best_idx >= 0) {
     // the hit record the Trace/shade step needs (raytracer.cpp:293-303): the same
     // primitive test with attributes, on the primitive this lane just tested (cached)
     const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
@@ -551,7 +576,8 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // becomes the lane's item (a leaf item waits for the next leaf phase).
 //
 // Per axis the ray's direction sign picks which of the two code words holds the near planes
-// of all four children (inv > 0: lo, else hi), so each child needs one max3 and one min3
+// of all four children (inv > 0: lo, else hi; one v_perm_b32 with a per-ray byte selector,
+// operands swapped for the far word), so each child needs one max3 and one min3
 // instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
 // always miss; child entries come precomputed from the host (node index, or the encoded
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
@@ -571,9 +597,10 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
   const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
   const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
-  const uint32_t nxw = (q.sgn & 1u) ? qa.y : qa.x, fxw = (q.sgn & 1u) ? qa.x : qa.y;
-  const uint32_t nyw = (q.sgn & 2u) ? qa.w : qa.z, fyw = (q.sgn & 2u) ? qa.z : qa.w;
-  const uint32_t nzw = (q.sgn & 4u) ? qb.y : qb.x, fzw = (q.sgn & 4u) ? qb.x : qb.y;
+  // perm(hi, lo, sel) is the near word; swapping the operands gives the far one
+  const uint32_t nxw = __builtin_amdgcn_perm(qa.y, qa.x, q.sel[0]), fxw = __builtin_amdgcn_perm(qa.x, qa.y, q.sel[0]);
+  const uint32_t nyw = __builtin_amdgcn_perm(qa.w, qa.z, q.sel[1]), fyw = __builtin_amdgcn_perm(qa.z, qa.w, q.sel[1]);
+  const uint32_t nzw = __builtin_amdgcn_perm(qb.y, qb.x, q.sel[2]), fzw = __builtin_amdgcn_perm(qb.x, qb.y, q.sel[2]);
   const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
   auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
   auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };

@@ -39,7 +39,7 @@ def main() -> None:
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     # regex on the mangled name; the default excludes the instrumented (kCount=true) variant
-    ap.add_argument("--kernel", default=r"trace_kernel(ILb0E|<false)")
+    ap.add_argument("--kernel", default=r"trace_(refill_)?kernel(ILb0E|<false)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--label", default="")
     a = ap.parse_args()
