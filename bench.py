@@ -37,6 +37,7 @@ METRIC = "Mrays/sec (primary+secondary), 1024x1024 @100spp; % HBM roofline"
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate over 8 XCDs
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 NODE_BYTES, PRIM_BYTES = 32, 64  # BASELINE.md / SURVEY.md 8(d) algorithmic bytes
+PMC_PROFILE = "r01_v14"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
@@ -66,8 +67,12 @@ def parse():
                     help="SURVEY.md 8(d) C2 BVH-stress variant: the soup without lights (one ray per sample)")
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="concurrent reference processes for the all-cores CPU figure (<= 1: skip)")
-    ap.add_argument("--pmc-traffic", default=os.path.join(ROOT, "profiles", "r01_v13_pmc_traffic.json"),
-                    help="JSON with per-launch HBM bytes of trace_kernel from rocprofv3 --pmc (tools/pmc_traffic.py)")
+    ap.add_argument("--pmc-traffic", default=None,
+                    help="JSON with per-launch HBM bytes of the trace kernel (tools/pmc_traffic.py); default: the "
+                         "committed profile of the headline workload, attached to that workload only")
+    ap.add_argument("--pmc-valu", default=None,
+                    help="JSON with the trace kernel's VALU issue fraction / lane utilisation (tools/pmc_valu.py); "
+                         "default as --pmc-traffic")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")
     return ap.parse_args()
@@ -276,11 +281,23 @@ def main():
     # HBM bytes per trace launch measured by rocprofv3 PMC passes of this same bench
     # (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE); committed with the kernel version
     # it was measured on (`label`)
-    traffic, traffic_src = None, None
-    if args.pmc_traffic and os.path.exists(args.pmc_traffic):
-        pm = json.load(open(args.pmc_traffic))
+    # it was measured on (`label`).  The committed profiles describe the headline workload
+    # only, so they are never attached to another scene's line.
+    headline = (args.scene is None and not args.primary_only and args.tris == 1_000_000 and args.res == 1024
+                and args.spp_sqrt == 10 and args.light_samples == 1 and args.emulate <= 1 and world == 1)
+    prof = os.path.join(ROOT, "profiles", PMC_PROFILE)
+    pmc_traffic = args.pmc_traffic or (prof + "_pmc_traffic.json" if headline else None)
+    pmc_valu = args.pmc_valu or (prof + "_pmc_valu.json" if headline else None)
+    traffic, traffic_src, valu = None, None, None
+    if pmc_traffic and os.path.exists(pmc_traffic):
+        pm = json.load(open(pmc_traffic))
         traffic = pm.get("hbm_bytes_per_launch")
-        traffic_src = f"{os.path.relpath(args.pmc_traffic, ROOT)} ({pm.get('label', '')})"
+        traffic_src = f"{os.path.relpath(pmc_traffic, ROOT)} ({pm.get('label', '')})"
+    if pmc_valu and os.path.exists(pmc_valu):
+        pv = json.load(open(pmc_valu))
+        valu = {"issue_frac": pv["valu_issue_frac"], "lane_utilisation": pv["lane_utilisation"],
+                "peak": "one wave64 VALU instruction per CU-cycle", "source": f"{os.path.relpath(pmc_valu, ROOT)} "
+                                                                             f"({pv.get('label', '')})"}
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(scene_path, args, rank)
@@ -309,13 +326,15 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_unit": "HBM bytes per trace launch", "traffic_source": traffic_src,
             "alg_bytes_per_launch": int(avg_launch_bytes),
-            "kernel": "trace_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
+            "kernel": "trace_refill_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
             "alg_bytes_per_ray": round(bytes_per_ray, 1), "launches_per_step": int(launches_all / args.steps),
             "trace_share_of_step": round(trace_ms_all / world / (elapsed * 1e3), 3),
             # the tree + primitives (~0.1 GB) stay on-die: algorithmic bytes are served by L2 /
             # Infinity Cache, so frac (vs HBM) can pass 1; the on-die ceiling is the L2's
             "l2_peak": L2_PEAK_GBS, "frac_of_l2": round(achieved / L2_PEAK_GBS, 4),
             "hbm_rate": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
+            # what actually binds the traversal: VALU issue (PMC pass)
+            "valu": valu,
         },
         "cpu_baseline": cpu,
     }

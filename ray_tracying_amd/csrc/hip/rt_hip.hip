@@ -6,19 +6,20 @@
 //                 reference's Trace -> shade recursion for that sample as an explicit state
 //                 machine whose state lives in SoA HBM buffers between steps; consumes the
 //                 previous query's answer and advances until the slot needs the next scene
-//                 query, which it appends to a compact query list.  A finished sample writes
-//                 its colour to the sample buffer and the slot pulls the next (pixel, sample)
-//                 unit from an atomic counter (64 consecutive units = 64 samples of one pixel:
-//                 maximally coherent rays per wave).
+//                 query, which it writes to the slot's query record.  A finished sample writes
+//                 its colour to the sample buffer; when all 64 slots of a wave are done the
+//                 wave claims the next batch of 64 consecutive units (one pixel's samples:
+//                 coherent rays) from sharded counters, one 128-B line each.
 //   reduce_kernel one thread per pixel (samples staged through LDS): compute_pixel_color sum over the s*s samples in
 //                 the reference's order, then the division (raytracer.cpp:46-69).
-//   trace_kernel  one thread per query.  BVH::get_intersection (acceleration.cpp:142):
+//   trace_refill_kernel  one lane per query.  BVH::get_intersection (acceleration.cpp:142):
 //                 closest-hit for camera/reflection/refraction rays, any-hit-within-tmax for
 //                 shadow rays (== the reference's `!hit.shape || t > light_dist`,
-//                 raytracer.cpp:233).  Persistent waves of 64 consecutive slots (one pixel
-//                 batch: coherent rays), 4-wide BVH with 64-B nodes (8-bit conservative
-//                 child grids), leaves tested first, near-first order with t-pruning,
-//                 per-lane stack in LDS (lane-minor -> conflict-free) with HBM spill.
+//                 raytracer.cpp:233).  Persistent waves; a lane whose query finished takes a
+//                 new one when fewer than 48 of 64 still traverse; 4-wide BVH with 64-B nodes
+//                 (8-bit conservative child grids), near-first order with t-pruning over an
+//                 (entry, t_near) stack in LDS (lane-minor, HBM spill), leaves postponed until
+//                 enough lanes wait on one.
 //
 // Splitting them keeps the heavy recursion/shading state out of the traversal's registers
 // (fused, the allocator needed ~250 VGPRs = 1 wave/SIMD).  Leaf boxes are tested with the
@@ -58,6 +59,10 @@ constexpr int kCtlBytes = 4096;    // control block; per-step reset region at by
 // atomics on one line serialise at the memory side, so the shards must not share lines.
 constexpr int kMaxBatchShards = 1024;
 constexpr int kCtrStride = 32;
+// Host batches: up to this many logic -> trace steps are enqueued before the host waits and
+// reads their any_query copies.  Steps after the frame's last query find every slot-wave
+// retired (logic) and no query (trace) and return at once, so a batch may overshoot.
+constexpr int kMaxHostBatch = 16;
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
@@ -296,118 +301,6 @@ __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query&
   return true;
 }
 
-// One 4-wide node visit: leaf children's primitives tested first, internal children pushed
-// far-to-near, `node` becomes the nearest one (or the popped stack top, or -1).
-template <bool kCount, bool kPlanesOnly>
-__device__ __forceinline__ void node_step(const TraceArgs& a, const Query& q, HitState& h, int& node, int& sp,
-                                          int* lstack, int gtid, unsigned int& nbox, unsigned int& nprim,
-                                          unsigned long long& dg_any_box, unsigned int& nvisit) {
-  const Ray& r = q.r;
-  const V3& inv = q.inv;
-  const bool any = q.any;
-  const float tmax = q.tmax;
-  // 64-B node, 8-bit child grids (rt_hip.h).  Slab entry/exit along x for child k:
-  // (origin + q*step - o) * inv == q * (step*inv) + (origin - o)*inv, evaluated as one
-  // packed fma per pair of children: culling only -- the boxes carry 1e-5*scale padding
-  // and every candidate hit is re-checked exactly (ref_leaf_ok + the primitive test).
-  const float4* nd = a.c.nodes + (size_t)node * 4;
-  const float4 g = nd[0];
-  const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
-  const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
-  const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
-  const uint32_t ex = __float_as_uint(g.w);
-  const uint32_t meta = qb.z;
-  const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
-  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
-  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
-  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
-  const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
-  auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
-  auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };
-  const f32x2 t_lx01 = __builtin_elementwise_fma(lo2(qa.x), Bx, Ax), t_lx23 = __builtin_elementwise_fma(hi2(qa.x), Bx, Ax);
-  const f32x2 t_hx01 = __builtin_elementwise_fma(lo2(qa.y), Bx, Ax), t_hx23 = __builtin_elementwise_fma(hi2(qa.y), Bx, Ax);
-  const f32x2 t_ly01 = __builtin_elementwise_fma(lo2(qa.z), By, Ay), t_ly23 = __builtin_elementwise_fma(hi2(qa.z), By, Ay);
-  const f32x2 t_hy01 = __builtin_elementwise_fma(lo2(qa.w), By, Ay), t_hy23 = __builtin_elementwise_fma(hi2(qa.w), By, Ay);
-  const f32x2 t_lz01 = __builtin_elementwise_fma(lo2(qb.x), Bz, Az), t_lz23 = __builtin_elementwise_fma(hi2(qb.x), Bz, Az);
-  const f32x2 t_hz01 = __builtin_elementwise_fma(lo2(qb.y), Bz, Az), t_hz23 = __builtin_elementwise_fma(hi2(qb.y), Bz, Az);
-  const float tx1[4] = {t_lx01.x, t_lx01.y, t_lx23.x, t_lx23.y}, tx2[4] = {t_hx01.x, t_hx01.y, t_hx23.x, t_hx23.y};
-  const float ty1[4] = {t_ly01.x, t_ly01.y, t_ly23.x, t_ly23.y}, ty2[4] = {t_hy01.x, t_hy01.y, t_hy23.x, t_hy23.y};
-  const float tz1[4] = {t_lz01.x, t_lz01.y, t_lz23.x, t_lz23.y}, tz2[4] = {t_hz01.x, t_hz01.y, t_hz23.x, t_hz23.y};
-  float tn[4];
-  bool hit[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float n0 = fmaxf(fmaxf(fminf(tx1[k], tx2[k]), fminf(ty1[k], ty2[k])), fminf(tz1[k], tz2[k]));
-    const float f0 = fminf(fminf(fmaxf(tx1[k], tx2[k]), fmaxf(ty1[k], ty2[k])), fmaxf(tz1[k], tz2[k]));
-    tn[k] = n0;
-    hit[k] = ((meta >> (8 * k)) & 0xffu) != 0 && n0 <= f0 && f0 >= 0.0f;
-  }
-  if (kCount) {
-    const uint64_t wm = __ballot(1);
-    if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
-    ++nvisit;
-    const unsigned nb = __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
-                                            (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
-    nbox += nb;
-    if (any) dg_any_box += nb;
-  }
-  // leaves first (their hits tighten the bound before internal children are ordered);
-  // one primitive-test instance walks the leaf bitmask (no 4x inlined copies)
-  uint32_t leaves = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (hit[k] && ((meta >> (8 * k)) & 0x80u)) {
-      leaves |= 1u << k;
-      hit[k] = false;
-    }
-  }
-  while (leaves != 0u) {
-    const int k = __builtin_ctz(leaves);
-    leaves &= leaves - 1u;
-    const float tk = k == 0 ? tn[0] : k == 1 ? tn[1] : k == 2 ? tn[2] : tn[3];
-    const int ck = (int)(((uint32_t)(k == 0 ? cc[0] : k == 1 ? cc[1] : k == 2 ? cc[2] : cc[3]) & 0x7fffffffu) >> 7);
-    float lim = any ? tmax : h.best_t;
-    lim = lim + (lim * 1e-5f + a.c.eps_abs);
-    if (!(tk > lim))
-      test_prims<kCount, kPlanesOnly>(a, ck, (int)((meta >> (8 * k)) & 0x7fu), r, any, tmax, q.par, true, h, nprim);
-    if (h.done) break;
-  }
-  if (h.done) {
-    node = -1;
-    return;
-  }
-  float lim = any ? tmax : h.best_t;
-  lim = lim + (lim * 1e-5f + a.c.eps_abs);
-  float t0 = __builtin_inff(), t1 = __builtin_inff(), t2 = __builtin_inff(), t3 = __builtin_inff();
-  int c0 = -1, c1 = -1, c2 = -1, c3 = -1;
-  if (hit[0] && !(tn[0] > lim)) { t0 = tn[0]; c0 = cc[0]; }
-  if (hit[1] && !(tn[1] > lim)) { t1 = tn[1]; c1 = cc[1]; }
-  if (hit[2] && !(tn[2] > lim)) { t2 = tn[2]; c2 = cc[2]; }
-  if (hit[3] && !(tn[3] > lim)) { t3 = tn[3]; c3 = cc[3]; }
-  // sort 4 (t, child) ascending; misses (-1, inf) sink to the end
-  cswap(t0, c0, t1, c1);
-  cswap(t2, c2, t3, c3);
-  cswap(t0, c0, t2, c2);
-  cswap(t1, c1, t3, c3);
-  cswap(t1, c1, t2, c2);
-  auto push = [&](int v) {
-    if (sp < a.lds_entries) lstack[sp * kBlock] = v;
-    else a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = v;
-    ++sp;
-  };
-  if (c3 >= 0) push(c3);
-  if (c2 >= 0) push(c2);
-  if (c1 >= 0) push(c1);
-  if (c0 >= 0) {
-    node = c0;
-  } else if (sp > 0) {
-    --sp;
-    node = sp < a.lds_entries ? lstack[sp * kBlock] : a.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid];
-  } else {
-    node = -1;
-  }
-}
-
 // After the traversal: the primitives whose region could not be boxed, then the result
 // word and (closest hits) the hit record the logic step shades.
 template <bool kCount, bool kPlanesOnly>
@@ -475,56 +368,6 @@ __device__ __forceinline__ void trace_counters_out(const TraceArgs& ta, int lane
       atomicAdd(ta.counters + 59, v);  // lane-level node visits
     }
   }
-}
-
-// Batch kernel: a wave traces 64 consecutive slots to completion, then pulls the next 64.
-// 4 waves/SIMD (<= 128 VGPRs, no spills); 5 waves needs 96 VGPRs and spills in the leaf path
-template <bool kCount, bool kPlanesOnly>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void trace_kernel(TraceArgs ta) {
-  extern __shared__ __attribute__((aligned(16))) int lds_stack[];
-  const unsigned int nq = (unsigned)ta.n_slots;
-  const int lane = threadIdx.x & 63;
-  unsigned int nrays = 0;
-  const int gtid = blockIdx.x * kBlock + threadIdx.x;
-  unsigned int nbox = 0, nprim = 0, nvisit = 0;
-  unsigned long long dg_any_rays = 0, dg_any_box = 0;  // kCount diagnostics: shadow (any-hit) queries
-  const TraceArgs& a = ta;
-  if (*ta.any_query == 0u) return;  // no slot emitted a query this step
-  // The slots are cut into fetch_shards slices with a counter each (one device-wide counter
-  // serialises at ~12 ns per 64-slot fetch: 1.6 ms per 8M-slot launch); a wave drains the
-  // slice of its block (blockIdx % 8 ~ its XCD) first, then helps the others.
-  const unsigned nfs = (unsigned)ta.fetch_shards;
-  const unsigned shard_len = (((nq + nfs - 1) / nfs) + 63u) & ~63u;
-  for (int sk = 0; sk < (int)nfs; ++sk) {
-   const int sh = (int)((blockIdx.x + sk) % nfs);
-   const unsigned sh_start = (unsigned)sh * shard_len;
-   if (sh_start >= nq) continue;
-   const unsigned sh_len = min(shard_len, nq - sh_start);
-   unsigned int* ctr = ta.fetch + sh * kFetchStride;
-   for (;;) {  // persistent: each wave pulls 64 queries at a time
-    unsigned int base = 0;
-    if (lane == 0) base = atomicAdd(ctr, 64u);
-    base = __shfl(base, 0);
-    if (base >= sh_len) break;
-    if (base + lane >= sh_len) continue;
-    const int slot = (int)(sh_start + base + lane);
-    Query q;
-    if (!begin_query(a, slot, q)) continue;  // no query from this slot in this step
-    ++nrays;
-    if (kCount && q.any) ++dg_any_rays;
-    HitState h{__builtin_inff(), 0x7fffffff, -1, false};
-    if (a.c.n_prims > 0 && !a.c.use_bvh) {  // BVH::intersect_linear (acceleration.cpp:124-139)
-      test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
-    } else if (a.c.n_prims > 0) {
-      int* lstack = lds_stack + threadIdx.x;
-      int sp = 0;
-      int node = a.n_nodes > 0 ? 0 : -1;
-      while (node >= 0) node_step<kCount, kPlanesOnly>(a, q, h, node, sp, lstack, gtid, nbox, nprim, dg_any_box, nvisit);
-    }
-    finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
-   }
-  }
-  trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
 }
 
 // ---- refill kernel with postponed leaves
@@ -1311,24 +1154,14 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
   if (planes) hipLaunchKernelGGL((logic_kernel<F, T, true>), dim3(blocks), dim3(kBlock), 0, st, la);
   else hipLaunchKernelGGL((logic_kernel<F, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
 }
-// trace launch: the refill kernel (default) or the fixed-batch kernel (RT_REFILL=0)
+// trace launch (the refill kernel; count: the instrumented variant)
 void launch_trace(const TraceArgs& ta, bool count, bool planes, unsigned blocks, size_t lds, hipStream_t st) {
-  if (ta.refill_min > 0) {
-    if (count) {
-      if (planes) hipLaunchKernelGGL((trace_refill_kernel<true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-      else hipLaunchKernelGGL((trace_refill_kernel<true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    } else {
-      if (planes) hipLaunchKernelGGL((trace_refill_kernel<false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-      else hipLaunchKernelGGL((trace_refill_kernel<false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    }
+  if (count) {
+    if (planes) hipLaunchKernelGGL((trace_refill_kernel<true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    else hipLaunchKernelGGL((trace_refill_kernel<true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   } else {
-    if (count) {
-      if (planes) hipLaunchKernelGGL((trace_kernel<true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-      else hipLaunchKernelGGL((trace_kernel<true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    } else {
-      if (planes) hipLaunchKernelGGL((trace_kernel<false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-      else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    }
+    if (planes) hipLaunchKernelGGL((trace_refill_kernel<false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    else hipLaunchKernelGGL((trace_refill_kernel<false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   }
 }
 static int fetch_shards_env() {
@@ -1355,7 +1188,7 @@ static int leaf_min_env() {
 static int refill_min_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_REFILL");
-    return e ? std::max(0, std::min(64, std::atoi(e))) : 48;
+    return e ? std::max(1, std::min(64, std::atoi(e))) : 48;
   }();
   return v;
 }
@@ -1422,10 +1255,12 @@ struct rt_scene_s {
   float* d_hit = nullptr;
   unsigned int* d_wave_done = nullptr;
   size_t slots_cap = 0;
-  unsigned int* h_flag = nullptr;  // pinned
+  unsigned int* h_flag = nullptr;  // pinned: one 128-B line per step of a host batch (any_query copies)
   unsigned int* d_batch_ctr = nullptr;  // kMaxBatchShards counters, one 128-B line each
   unsigned int* d_fetch = nullptr;      // trace fetch counters (one line each) + any_query line
-  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_a = nullptr, ev_b = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
+  hipEvent_t ev_a[kMaxHostBatch] = {}, ev_b[kMaxHostBatch] = {};  // per step of a host batch: around the trace launch
+  int last_iters = 0;  // steps the previous render took: the size of the next render's first host batch
 };
 
 static void free_workspace(rt_scene_s* s) {
@@ -1478,9 +1313,13 @@ int rt_scene_destroy(rt_scene_t s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
-  hipEvent_t evs[] = {s->ev_t0, s->ev_t1, s->ev_a, s->ev_b};
+  hipEvent_t evs[] = {s->ev_t0, s->ev_t1};
   for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
+  for (int k = 0; k < kMaxHostBatch; ++k) {
+    if (s->ev_a[k]) (void)hipEventDestroy(s->ev_a[k]);
+    if (s->ev_b[k]) (void)hipEventDestroy(s->ev_b[k]);
+  }
   delete s;
   return RT_OK;
 }
@@ -1534,11 +1373,14 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     rt_scene_destroy(s);
     return rc;
   }
-  if (hipMalloc(&s->d_ctl, kCtlBytes) != hipSuccess || hipHostMalloc((void**)&s->h_flag, 64) != hipSuccess ||
+  bool ev_ok = true;
+  for (int k = 0; k < kMaxHostBatch && ev_ok; ++k)
+    ev_ok = hipEventCreate(&s->ev_a[k]) == hipSuccess && hipEventCreate(&s->ev_b[k]) == hipSuccess;
+  if (!ev_ok || hipMalloc(&s->d_ctl, kCtlBytes) != hipSuccess ||
+      hipHostMalloc((void**)&s->h_flag, (size_t)kMaxHostBatch * kFetchStride * 4) != hipSuccess ||
       hipMalloc(&s->d_batch_ctr, (size_t)kMaxBatchShards * kCtrStride * 4) != hipSuccess ||
       hipMalloc(&s->d_fetch, ((size_t)kMaxFetchShards + 1) * kFetchStride * 4) != hipSuccess ||
-      hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
-      hipEventCreate(&s->ev_a) != hipSuccess || hipEventCreate(&s->ev_b) != hipSuccess) {
+      hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess) {
     rt_scene_destroy(s);
     return fail(RT_ENOMEM, "rt_scene_create: control block / events");
   }
@@ -1546,11 +1388,9 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const int lds_entries = std::min(d->stack_bound, lds_stack_entries());
-    const bool refill = refill_min_env() > 0;
     const bool planes = d->prim_stride == 64;
-    const void* fn = refill ? (planes ? (const void*)trace_refill_kernel<false, true> : (const void*)trace_refill_kernel<false, false>)
-                            : (planes ? (const void*)trace_kernel<false, true> : (const void*)trace_kernel<false, false>);
-    const size_t lds_bytes = (size_t)lds_entries * kBlock * (refill ? 2 * sizeof(int) : sizeof(int));
+    const void* fn = planes ? (const void*)trace_refill_kernel<false, true> : (const void*)trace_refill_kernel<false, false>;
+    const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kBlock, lds_bytes) != hipSuccess || bpc < 1)
       bpc = 2;
     if (const char* e = std::getenv("RT_TRACE_BPC")) bpc = std::max(1, std::min(bpc, std::atoi(e)));  // diagnostic
@@ -1712,8 +1552,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   }
   ta.spill = s->d_spill;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
-  // refill kernel: entry + t_near per stack slot
-  const size_t lds = (size_t)ta.lds_entries * kBlock * (ta.refill_min > 0 ? 2 * sizeof(int) : sizeof(int));
+  // entry + t_near per stack slot
+  const size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result,
@@ -1727,35 +1567,42 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
   unsigned long long diag_prev = 0;
   if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
+  // steps go out in host batches (one wait per batch, not per step); the first batch is
+  // sized by the previous render's step count, the diagnostics wait on every step
+  const bool step_sync = diag || replay_iter >= 0;
+  int batch = step_sync ? 1 : std::max(2, std::min(kMaxHostBatch, s->last_iters + 1));
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
-  for (;;) {
-    // per-step reset: trace work counters (byte 2048) + any_query (byte 3072)
+  for (bool done = false; !done;) {
+   for (int k = 0; k < batch; ++k) {
     // per-step reset: trace work counters + any_query (the line after them)
     HIP_TRY(hipMemsetAsync(s->d_fetch, 0, ((size_t)ta.fetch_shards + 1) * kFetchStride * 4, stream), RT_EDEVICE);
     launch_logic(la, need_frames, (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0, planes_only, slot_blocks, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipMemcpyAsync(s->h_flag, la.any_query, 4, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
-    HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
+    HIP_TRY(hipMemcpyAsync(s->h_flag + (size_t)k * kFetchStride, la.any_query, 4, hipMemcpyDeviceToHost, stream),
+            RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_a[k], stream), RT_EDEVICE);
     launch_trace(ta, p->count_work != 0, planes_only, trace_blocks, lds, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
-    HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_b[k], stream), RT_EDEVICE);
+   }
+   HIP_TRY(hipEventSynchronize(s->ev_b[batch - 1]), RT_EDEVICE);
+   for (int k = 0; k < batch && !done; ++k) {
     float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->ev_a, s->ev_b), RT_EDEVICE);
-    if (replay_iter == iters && replay_reps > 0 && !p->count_work) {
+    HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[k], s->ev_b[k]), RT_EDEVICE);
+    if (replay_iter == iters && replay_reps > 0 && !p->count_work) {  // batch == 1 here
       // diagnostic (RT_TRACE_REPLAY=iter:reps): re-trace this step's queries; the results
       // are recomputed identically, so the frame is unchanged
       float tot = 0.f, best = 1e30f;
       unsigned long long rays0 = 0;
       HIP_TRY(hipMemcpy(&rays0, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-      for (int k = 0; k < replay_reps; ++k) {
+      for (int r = 0; r < replay_reps; ++r) {
         HIP_TRY(hipMemsetAsync(s->d_fetch, 0, (size_t)ta.fetch_shards * kFetchStride * 4, stream), RT_EDEVICE);
-        HIP_TRY(hipEventRecord(s->ev_a, stream), RT_EDEVICE);
+        HIP_TRY(hipEventRecord(s->ev_a[1], stream), RT_EDEVICE);
         launch_trace(ta, false, planes_only, trace_blocks, lds, stream);
-        HIP_TRY(hipEventRecord(s->ev_b, stream), RT_EDEVICE);
-        HIP_TRY(hipEventSynchronize(s->ev_b), RT_EDEVICE);
+        HIP_TRY(hipEventRecord(s->ev_b[1], stream), RT_EDEVICE);
+        HIP_TRY(hipEventSynchronize(s->ev_b[1]), RT_EDEVICE);
         float m = 0.f;
-        HIP_TRY(hipEventElapsedTime(&m, s->ev_a, s->ev_b), RT_EDEVICE);
+        HIP_TRY(hipEventElapsedTime(&m, s->ev_a[1], s->ev_b[1]), RT_EDEVICE);
         tot += m;
         best = std::min(best, m);
       }
@@ -1765,7 +1612,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       std::fprintf(stderr, "[rt replay] step %d: %llu queries, trace %.4f ms avg / %.4f ms min over %d reps\n", iters,
                    (rays1 - rays0) / (unsigned long long)replay_reps, tot / replay_reps, best, replay_reps);
     }
-    const bool more = *s->h_flag != 0;
+    const bool more = s->h_flag[(size_t)k * kFetchStride] != 0;
     if (diag && more) {
       unsigned long long rc = 0;
       HIP_TRY(hipMemcpy(&rc, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
@@ -1773,12 +1620,16 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
                    (double)(rc - diag_prev) / (ms * 1e6));
       diag_prev = rc;
     }
-    if (more) {  // the final (empty) trace launch is not a traversal step
+    if (more) {  // the final (empty) trace launch -- and any after it in the batch -- is not a traversal step
       trace_ms += ms;
       ++iters;
+    } else {
+      done = true;
     }
-    if (!more) break;
+   }
+   batch = step_sync ? 1 : 4;  // the previous render's count fell short: top up in small batches
   }
+  s->last_iters = iters;
   hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
   HIP_TRY(hipGetLastError(), RT_EDEVICE);
   HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);

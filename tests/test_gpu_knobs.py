@@ -1,0 +1,57 @@
+"""The scheduling knobs of the trace / logic kernels never change a result.
+
+Each knob is read once per process (environment), so every configuration renders in a fresh
+child process and must match the oracle bit for bit: the LDS traversal stack cut to 2
+entries (every deeper entry spills to HBM), extreme refill / leaf-phase thresholds, one and
+many work-counter shards, and a slot count so small that a frame takes dozens of steps.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import scenes
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import ray_tracying_amd as rt
+sc = rt.Scene(sys.argv[2], texture_root=sys.argv[4])
+img, st = sc.render(rt.RenderParams(spp_sqrt=2, light_samples=2, use_bvh=True, seed=5))
+np.save(sys.argv[3], img)
+print(st.rays)
+"""
+
+KNOBS = [
+    {"RT_LDS_STACK": "2"},
+    {"RT_LEAF_MIN": "1", "RT_REFILL": "64"},
+    {"RT_LEAF_MIN": "64", "RT_REFILL": "1"},
+    {"RT_BATCH_SHARDS": "1", "RT_FETCH_SHARDS": "64", "RT_SLOTS": "4096"},
+    {"RT_BATCH_SHARDS": "1024", "RT_FETCH_SHARDS": "1"},
+]
+
+
+@pytest.mark.parametrize("scene", ["soup", "features"])
+def test_knobs_do_not_change_results(scene, tmp_path, gpu):
+    if scene == "soup":
+        p = scenes.write(scenes.soup(3000, seed=11, res=(48, 48)), str(tmp_path / "s.json"))
+    else:  # reflection, refraction, soft shadows, textures, every primitive kind
+        p = scenes.write(scenes.features(res=(40, 32)), str(tmp_path / "f.json"))
+    ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=5, spp_sqrt=2, light_samples=2, use_bvh=True,
+                            texture_root=scenes.TEXTURES)
+    for i, env in enumerate(KNOBS):
+        out = str(tmp_path / f"img{i}.npy")
+        r = subprocess.run([sys.executable, "-c", CHILD, ROOT, p, out, scenes.TEXTURES],
+                           env={**os.environ, **env}, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (env, r.stderr[-2000:])
+        img = np.load(out)
+        diff = int((img.view(np.uint32) != ref.view(np.uint32)).sum())
+        assert diff == 0, f"{env}: {diff} channels differ"
+        assert int(r.stdout.strip().splitlines()[-1]) == ost["rays"], env
