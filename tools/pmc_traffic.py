@@ -8,6 +8,7 @@ DIR is the -d directory of a `rocprofv3 --pmc FETCH_SIZE` (resp. WRITE_SIZE) run
 FETCH_SIZE counts 64 B per 128-B memory-side read request on gfx950, so it is doubled;
 WRITE_SIZE is taken as is.  Both counters are in KB (rocprofv3 derived counters).
 The two counters need separate passes (TCC slots: FETCH_SIZE 3, WRITE_SIZE 2 of 4).
+Dispatches shorter than 50 us (the empty launch that ends a frame) are left out.
 """
 from __future__ import annotations
 
@@ -19,7 +20,7 @@ import os
 import re
 
 
-def per_dispatch(root: str, counter: str, kernel: str) -> list[float]:
+def per_dispatch(root: str, counter: str, kernel: str, min_ns: int = 50_000) -> list[float]:
     vals: dict[tuple[str, str], float] = {}
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -28,6 +29,9 @@ def per_dispatch(root: str, counter: str, kernel: str) -> list[float]:
         with open(f, newline="") as fh:
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter or not re.search(kernel, row.get("Kernel_Name", "")):
+                    continue
+                # the frame's last launch finds no query and returns at once: not a traversal step
+                if "End_Timestamp" in row and int(row["End_Timestamp"]) - int(row["Start_Timestamp"]) < min_ns:
                     continue
                 key = (f, row.get("Dispatch_Id", row.get("Correlation_Id", "")))
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
