@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <utility>
 #include <stdexcept>
 #include <vector>
 
@@ -29,9 +30,13 @@ namespace rth {
 
 namespace {
 
+// spatial splits (SBVH-style): extra references allowed, as a fraction of the bounded
+// primitives (RT_SBVH_DUP; 0 = object splits only)
+constexpr double kSbvhDup = 0.3;
+
 struct BuildPrim {
-  Box box;
-  V3 c;  // centroid
+  Box box;  // padded box of the whole primitive
+  V3 c;     // centroid
   int id;
 };
 
@@ -41,57 +46,186 @@ inline float area(const Box& b) {
   return 2.0f * (dx * dy + dy * dz + dz * dx);
 }
 
+inline Box intersect(const Box& a, const Box& b) {
+  Box r;
+  for (int i = 0; i < 3; ++i) {
+    r.lo[i] = std::max(a.lo[i], b.lo[i]);
+    r.hi[i] = std::min(a.hi[i], b.hi[i]);
+  }
+  return r;
+}
+
 struct Node2 {
   Box box;
   int left = -1, right = -1;  // internal: children
-  int start = 0, count = 0;   // leaf: range in `order`
+  int start = 0, count = 0;   // leaf: range in `leaf_refs`
 };
+
+// A reference: a primitive, or the part of it inside `clip` (spatial splits).  `box` is the
+// padded box of the primitive's acceptance polygon clipped to `clip` -- every point the
+// primitive test can report inside `clip` (to within rounding) lies in `box`, and the parts
+// of one primitive cover its whole acceptance region, so near-first pruning stays exact.
+struct Ref {
+  Box box;
+  Box clip;  // accumulated split slabs (unpadded), initially unbounded
+  int p;     // index into the BuildPrim table
+};
+
+// Acceptance polygons of the planes (two triangles each, double; tri_region's vertices).
+// Primitives without one (spheres, cubes, rectangles, degenerate regions) are never split.
+struct Polys {
+  std::vector<double> v;    // 9 doubles per triangle
+  std::vector<int> off, n;  // per BuildPrim: first triangle, triangle count (0: no polygon)
+};
+
+// Sutherland-Hodgman against one axis-aligned plane: keeps x[axis] >= v (ge) or <= v.
+static int clip_plane(const double (*in)[3], int n, double (*out)[3], int axis, double v, bool ge) {
+  int m = 0;
+  for (int i = 0; i < n; ++i) {
+    const double* a = in[i];
+    const double* b = in[(i + 1) % n];
+    const double da = ge ? a[axis] - v : v - a[axis];
+    const double db = ge ? b[axis] - v : v - b[axis];
+    if (da >= 0) {
+      for (int k = 0; k < 3; ++k) out[m][k] = a[k];
+      ++m;
+    }
+    if ((da >= 0) != (db >= 0)) {
+      const double t = da / (da - db);
+      for (int k = 0; k < 3; ++k) out[m][k] = a[k] + t * (b[k] - a[k]);
+      out[m][axis] = v;
+      ++m;
+    }
+  }
+  return m;
+}
 
 struct SAHBuilder {
   std::vector<BuildPrim>& P;
+  const Polys& polys;
+  float pad_abs;  // 1e-5 * scene scale
   std::vector<Node2> nodes;
+  std::vector<Ref> leaf_refs;
   static constexpr int kBinsMax = 64;
   int kBins = 32;          // RT_SAH_BINS (tuning knob; 16 -> 32 and node 1.0 -> 0.5: +1.2%)
   int kMaxLeaf = 4;        // RT_SAH_LEAF
   float kNodeCost = 0.5f;  // RT_SAH_NODE: traversal step cost relative to one primitive test
+  float kSplitAlpha = 1e-5f;  // RT_SBVH_ALPHA: try spatial splits when children overlap > alpha * root area
+  long long dup_budget = 0;   // RT_SBVH_DUP: extra references allowed (fraction of the primitives)
+  float root_area = 0.0f;
 
-  int build(int start, int end, int depth) {
+  Box pad(Box b) const {
+    for (int i = 0; i < 3; ++i) {
+      b.lo[i] -= pad_abs + std::fabs(b.lo[i]) * 2e-6f;
+      b.hi[i] += pad_abs + std::fabs(b.hi[i]) * 2e-6f;
+    }
+    return b;
+  }
+
+  // the reference `r` restricted to clip `c`; false if nothing of the primitive is left
+  bool clipped(const Ref& r, const Box& c, Ref& out) const {
+    out.p = r.p;
+    out.clip = c;
+    const int nt = polys.n[r.p];
+    if (nt == 0) {  // no polygon: the whole box, trimmed to the padded slab
+      out.box = intersect(P[r.p].box, pad(c));
+      return true;
+    }
+    Box b;
+    bool any = false;
+    for (int t = 0; t < nt; ++t) {
+      double A[16][3], B[16][3];
+      const double* tv = &polys.v[(size_t)(polys.off[r.p] + t) * 9];
+      for (int k = 0; k < 3; ++k)
+        for (int m = 0; m < 3; ++m) A[k][m] = tv[k * 3 + m];
+      int n = 3;
+      for (int ax = 0; ax < 3 && n > 0; ++ax) {
+        if (std::isfinite(c.lo[ax])) {
+          n = clip_plane(A, n, B, ax, c.lo[ax], true);
+          for (int k = 0; k < n; ++k) std::memcpy(A[k], B[k], sizeof A[k]);
+        }
+        if (n > 0 && std::isfinite(c.hi[ax])) {
+          n = clip_plane(A, n, B, ax, c.hi[ax], false);
+          for (int k = 0; k < n; ++k) std::memcpy(A[k], B[k], sizeof A[k]);
+        }
+      }
+      for (int k = 0; k < n; ++k) {
+        b.merge(V3{(float)A[k][0], (float)A[k][1], (float)A[k][2]});
+        any = true;
+      }
+    }
+    if (!any) return false;
+    out.box = intersect(pad(b), P[r.p].box);
+    return true;
+  }
+
+  // binning of a spatial split: the reference's polygon cut at each bin plane in turn (the
+  // remainder carried on), each piece's padded box (within the reference's box) into its bin
+  void sweep_bins(const Ref& r, int ax, float lo, float w, int b0, int b1, Box* bb) const {
+    Box part[kBinsMax];
+    for (int t = 0; t < polys.n[r.p]; ++t) {
+      double A[16][3], L[16][3], Rm[16][3];
+      const double* tv = &polys.v[(size_t)(polys.off[r.p] + t) * 9];
+      for (int k = 0; k < 3; ++k)
+        for (int m = 0; m < 3; ++m) A[k][m] = tv[k * 3 + m];
+      int n = 3;
+      for (int k = b0; k < b1 && n > 0; ++k) {
+        const double plane = (double)lo + (double)w * (k + 1);
+        const int nl = clip_plane(A, n, L, ax, plane, false);
+        for (int q = 0; q < nl; ++q) part[k].merge(V3{(float)L[q][0], (float)L[q][1], (float)L[q][2]});
+        n = clip_plane(A, n, Rm, ax, plane, true);
+        for (int q = 0; q < n; ++q) std::memcpy(A[q], Rm[q], sizeof A[q]);
+      }
+      for (int q = 0; q < n; ++q) part[b1].merge(V3{(float)A[q][0], (float)A[q][1], (float)A[q][2]});
+    }
+    for (int k = b0; k <= b1; ++k)
+      if (part[k].lo[0] <= part[k].hi[0]) bb[k].merge(intersect(pad(part[k]), r.box));
+  }
+
+  int make_leaf(int id, std::vector<Ref>& refs) {
+    nodes[id].start = (int)leaf_refs.size();
+    nodes[id].count = (int)refs.size();
+    leaf_refs.insert(leaf_refs.end(), refs.begin(), refs.end());
+    return id;
+  }
+
+  int build(std::vector<Ref> refs, int depth) {
     int id = (int)nodes.size();
     nodes.emplace_back();
     Box b, cb;
-    for (int i = start; i < end; ++i) {
-      b.merge(P[i].box);
-      cb.merge(P[i].c);
+    for (const Ref& r : refs) {
+      b.merge(r.box);
+      cb.merge(V3{0.5f * (r.box.lo[0] + r.box.hi[0]), 0.5f * (r.box.lo[1] + r.box.hi[1]),
+                  0.5f * (r.box.lo[2] + r.box.hi[2])});
     }
     nodes[id].box = b;
-    const int n = end - start;
-    if (n <= 1 || depth > 60) {
-      nodes[id].start = start;
-      nodes[id].count = n;
-      if (n <= kMaxLeaf) return id;
-    }
-    // binned SAH over all three axes
+    if (depth == 0) root_area = area(b);
+    const int n = (int)refs.size();
+    if (n <= 1 || depth > 60) return make_leaf(id, refs);
+    auto centroid = [](const Ref& r, int ax) { return 0.5f * (r.box.lo[ax] + r.box.hi[ax]); };
+    // object split: binned SAH over all three axes
     float best_cost = INFINITY;
     int best_axis = -1, best_bin = -1;
+    Box best_l, best_r;
     for (int ax = 0; ax < 3; ++ax) {
       float lo = cb.lo[ax], hi = cb.hi[ax];
       if (!(hi > lo)) continue;
       float scale = kBins / (hi - lo);
       Box bb[kBinsMax];
       int cnt[kBinsMax] = {0};
-      for (int i = start; i < end; ++i) {
-        int k = std::min(kBins - 1, (int)((P[i].c[ax] - lo) * scale));
-        bb[k].merge(P[i].box);
+      for (const Ref& r : refs) {
+        int k = std::min(kBins - 1, (int)((centroid(r, ax) - lo) * scale));
+        bb[k].merge(r.box);
         cnt[k]++;
       }
-      float ra[kBinsMax];
+      Box rb[kBinsMax];
       int rc[kBinsMax];
       Box acc;
       int c = 0;
       for (int k = kBins - 1; k > 0; --k) {
         acc.merge(bb[k]);
         c += cnt[k];
-        ra[k] = area(acc);
+        rb[k] = acc;
         rc[k] = c;
       }
       Box accl;
@@ -100,34 +234,109 @@ struct SAHBuilder {
         accl.merge(bb[k]);
         cl += cnt[k];
         if (cl == 0 || rc[k + 1] == 0) continue;
-        float cost = area(accl) * cl + ra[k + 1] * rc[k + 1];
+        float cost = area(accl) * cl + area(rb[k + 1]) * rc[k + 1];
         if (cost < best_cost) {
           best_cost = cost;
           best_axis = ax;
           best_bin = k;
+          best_l = accl;
+          best_r = rb[k + 1];
+        }
+      }
+    }
+    // spatial split: bins over the node box, references clipped into every bin they span
+    int sp_axis = -1;
+    float sp_pos = 0.0f;
+    if (dup_budget > 0 && best_axis >= 0 && area(intersect(best_l, best_r)) > kSplitAlpha * root_area) {
+      for (int ax = 0; ax < 3; ++ax) {
+        const float lo = b.lo[ax], hi = b.hi[ax];
+        if (!(hi > lo)) continue;
+        const float w = (hi - lo) / kBins;
+        Box bb[kBinsMax];
+        int enter[kBinsMax] = {0}, leave[kBinsMax] = {0};
+        for (const Ref& r : refs) {
+          int b0 = std::min(kBins - 1, std::max(0, (int)((r.box.lo[ax] - lo) / w)));
+          int b1 = std::min(kBins - 1, std::max(0, (int)((r.box.hi[ax] - lo) / w)));
+          if (polys.n[r.p] == 0) b0 = b1 = std::min(kBins - 1, std::max(0, (int)((centroid(r, ax) - lo) / w)));
+          if (b0 == b1)
+            bb[b0].merge(r.box);
+          else
+            sweep_bins(r, ax, lo, w, b0, b1, bb);
+          enter[b0]++;
+          leave[b1]++;
+        }
+        Box rb[kBinsMax];
+        int rc[kBinsMax];
+        Box acc;
+        int c = 0;
+        for (int k = kBins - 1; k > 0; --k) {
+          acc.merge(bb[k]);
+          c += leave[k];
+          rb[k] = acc;
+          rc[k] = c;
+        }
+        Box accl;
+        int cl = 0;
+        for (int k = 0; k < kBins - 1; ++k) {
+          accl.merge(bb[k]);
+          cl += enter[k];
+          if (cl == 0 || rc[k + 1] == 0) continue;
+          float cost = area(accl) * cl + area(rb[k + 1]) * rc[k + 1];
+          if (cost < best_cost) {
+            best_cost = cost;
+            sp_axis = ax;
+            sp_pos = lo + w * (k + 1);
+          }
         }
       }
     }
     const float leaf_cost = area(b) * n;
     const float node_cost = area(b) * kNodeCost;  // traversal step relative to one primitive test
-    if (n <= kMaxLeaf && (best_axis < 0 || best_cost * 1.0f + node_cost >= leaf_cost)) {
-      nodes[id].start = start;
-      nodes[id].count = n;
-      return id;
+    if (n <= kMaxLeaf && ((best_axis < 0 && sp_axis < 0) || best_cost * 1.0f + node_cost >= leaf_cost))
+      return make_leaf(id, refs);
+    std::vector<Ref> L, R;
+    if (sp_axis >= 0) {
+      for (const Ref& r : refs) {
+        const bool poly = polys.n[r.p] != 0;
+        if (!poly) {
+          (centroid(r, sp_axis) < sp_pos ? L : R).push_back(r);
+          continue;
+        }
+        if (r.box.hi[sp_axis] <= sp_pos) { L.push_back(r); continue; }
+        if (r.box.lo[sp_axis] >= sp_pos) { R.push_back(r); continue; }
+        Box cl = r.clip, cr = r.clip;
+        cl.hi[sp_axis] = std::min(cl.hi[sp_axis], sp_pos);
+        cr.lo[sp_axis] = std::max(cr.lo[sp_axis], sp_pos);
+        Ref a, c;
+        const bool ha = clipped(r, cl, a), hc = clipped(r, cr, c);
+        if (ha) L.push_back(a);
+        if (hc) R.push_back(c);
+        if (ha && hc) --dup_budget;
+        if (!ha && !hc) L.push_back(r);  // cannot happen for a nonempty polygon; keep it anyway
+      }
+      if (L.empty() || R.empty()) {  // degenerate: fall back to the object split below
+        L.clear();
+        R.clear();
+        sp_axis = -1;
+      }
     }
-    int mid;
-    if (best_axis < 0) {  // all centroids coincide: split the index range
-      mid = start + n / 2;
-    } else {
-      float lo = cb.lo[best_axis], scale = kBins / (cb.hi[best_axis] - lo);
-      auto it = std::partition(P.begin() + start, P.begin() + end, [&](const BuildPrim& p) {
-        return std::min(kBins - 1, (int)((p.c[best_axis] - lo) * scale)) <= best_bin;
-      });
-      mid = (int)(it - P.begin());
-      if (mid == start || mid == end) mid = start + n / 2;
+    if (sp_axis < 0) {
+      if (best_axis < 0) {  // all centroids coincide: split the list
+        L.assign(refs.begin(), refs.begin() + n / 2);
+        R.assign(refs.begin() + n / 2, refs.end());
+      } else {
+        float lo = cb.lo[best_axis], scale = kBins / (cb.hi[best_axis] - lo);
+        for (const Ref& r : refs)
+          (std::min(kBins - 1, (int)((centroid(r, best_axis) - lo) * scale)) <= best_bin ? L : R).push_back(r);
+        if (L.empty() || R.empty()) {
+          L.assign(refs.begin(), refs.begin() + n / 2);
+          R.assign(refs.begin() + n / 2, refs.end());
+        }
+      }
     }
-    int l = build(start, mid, depth + 1);
-    int r = build(mid, end, depth + 1);
+    std::vector<Ref>().swap(refs);
+    int l = build(std::move(L), depth + 1);
+    int r = build(std::move(R), depth + 1);
     nodes[id].left = l;
     nodes[id].right = r;
     nodes[id].count = 0;
@@ -142,7 +351,7 @@ struct SAHBuilder {
 // triangle (possibly empty) whose vertices are pairwise line intersections.  Works for either
 // winding.  Returns false if the region is unbounded (parallel / zero-length edges).
 bool tri_region(const double A[3], const double B[3], const double C[3], const double n[3], double tol,
-                Box& box, bool& nonempty) {
+                Box& box, bool& nonempty, std::vector<double>* verts = nullptr) {
   auto sub = [](const double* a, const double* b, double* o) { o[0] = a[0] - b[0]; o[1] = a[1] - b[1]; o[2] = a[2] - b[2]; };
   auto cross = [](const double* a, const double* b, double* o) {
     o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
@@ -190,6 +399,8 @@ bool tri_region(const double A[3], const double B[3], const double C[3], const d
     V3 P;
     for (int m = 0; m < 3; ++m) P[m] = (float)(A[m] + a * u[m] + b * v[m]);
     box.merge(P);
+    if (verts)
+      for (int m = 0; m < 3; ++m) verts->push_back(A[m] + a * u[m] + b * v[m]);
   }
   return true;
 }
@@ -266,12 +477,14 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
   std::vector<uint8_t> has_accept(n, 0);
   std::vector<int> unbounded;  // sorted positions
   std::vector<int> never;      // planes that accept no point: kept for indexing, never traversed
+  Polys polys;                 // per bounded primitive: acceptance triangles (spatial splits)
   bounded.reserve(n);
   for (int r = 0; r < n; ++r) {
     const Shape& s = sc.shapes[sc.order[r]];
     Box b = shape_box[sc.order[r]];
     bool ok = true;
     float pad = margin;
+    std::vector<double> tv1, tv2;  // the two sub-triangles' acceptance regions (3 vertices each)
     if (s.kind == RT_PRIM_PLANE) {
       // isPointInQuad = triangle (c1,c3,c2) OR triangle (c0,c1,c2) (shapes.cpp:485-494); the
       // acceptance regions (2x the reference's 1e-6 tolerance for float rounding) bound every
@@ -292,7 +505,8 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
       for (double& x : nn) x /= ln;
       Box region;
       bool ne1 = false, ne2 = false;
-      ok = tri_region(C[1], C[3], C[2], nn, 2e-6, region, ne1) && tri_region(C[0], C[1], C[2], nn, 2e-6, region, ne2);
+      ok = tri_region(C[1], C[3], C[2], nn, 2e-6, region, ne1, &tv1) &&
+           tri_region(C[0], C[1], C[2], nn, 2e-6, region, ne2, &tv2);
       if (ok && !ne1 && !ne2) { never.push_back(r); continue; }  // accepts nothing
       if (ok) {
         b = region;
@@ -309,23 +523,57 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
       unbounded.push_back(r);
       continue;
     }
+    // polygons only when both regions are whole triangles or empty (otherwise: never split)
+    int ntri = 0;
+    if ((tv1.size() == 9 || tv1.empty()) && (tv2.size() == 9 || tv2.empty()) && !(tv1.empty() && tv2.empty())) {
+      // c3 == c0 makes both sub-triangles the same triangle: keep one copy
+      bool same = tv1.size() == 9 && tv2.size() == 9;
+      for (int k = 0; k < 3 && same; ++k) {
+        bool found = false;
+        for (int m = 0; m < 3 && !found; ++m)
+          found = std::fabs(tv1[k * 3] - tv2[m * 3]) + std::fabs(tv1[k * 3 + 1] - tv2[m * 3 + 1]) +
+                      std::fabs(tv1[k * 3 + 2] - tv2[m * 3 + 2]) <= 1e-12 * (1.0 + std::fabs(tv1[k * 3]));
+        same = found;
+      }
+      polys.off.push_back((int)(polys.v.size() / 9));
+      polys.v.insert(polys.v.end(), tv1.begin(), tv1.end());
+      if (!same) polys.v.insert(polys.v.end(), tv2.begin(), tv2.end());
+      ntri = (int)(polys.v.size() / 9) - polys.off.back();
+    } else {
+      polys.off.push_back((int)(polys.v.size() / 9));
+    }
+    polys.n.push_back(ntri);
     BuildPrim bp;
     bp.box = b;
     bp.c = {0.5f * (b.lo[0] + b.hi[0]), 0.5f * (b.lo[1] + b.hi[1]), 0.5f * (b.lo[2] + b.hi[2])};
     bp.id = r;
     bounded.push_back(bp);
   }
-  SAHBuilder B{bounded, {}};
+  SAHBuilder B{bounded, polys, margin, {}, {}};
   if (const char* e = std::getenv("RT_SAH_BINS")) B.kBins = std::max(2, std::min(SAHBuilder::kBinsMax, std::atoi(e)));
   if (const char* e = std::getenv("RT_SAH_LEAF")) B.kMaxLeaf = std::max(1, std::min(15, std::atoi(e)));
   if (const char* e = std::getenv("RT_SAH_NODE")) B.kNodeCost = (float)std::atof(e);
+  if (const char* e = std::getenv("RT_SBVH_ALPHA")) B.kSplitAlpha = (float)std::atof(e);
+  double dup = kSbvhDup;
+  if (const char* e = std::getenv("RT_SBVH_DUP")) dup = std::max(0.0, std::min(4.0, std::atof(e)));
+  B.dup_budget = (long long)(dup * (double)bounded.size());
   B.nodes.reserve(bounded.size() + 1);
-  if (!bounded.empty()) B.build(0, (int)bounded.size(), 0);
+  if (!bounded.empty()) {
+    std::vector<Ref> refs(bounded.size());
+    Box open;  // no clip yet
+    for (int a = 0; a < 3; ++a) {
+      open.lo[a] = -INFINITY;
+      open.hi[a] = INFINITY;
+    }
+    for (size_t i = 0; i < bounded.size(); ++i) refs[i] = Ref{bounded[i].box, open, (int)i};
+    B.build(std::move(refs), 0);
+  }
 
-  // new primitive order: leaves of the SAH tree (DFS), then the unbounded list
+  // new primitive order: leaf references of the SAH tree (DFS; a primitive split by spatial
+  // splits appears once per part), then the never-hit and the unbounded lists
   std::vector<int> new_order;  // new index -> sorted reference position r
-  new_order.reserve(n);
-  for (auto& bp : bounded) new_order.push_back(bp.id);  // leaves are contiguous ranges of `bounded`
+  new_order.reserve(B.leaf_refs.size() + never.size() + unbounded.size());
+  for (const Ref& r : B.leaf_refs) new_order.push_back(bounded[r.p].id);
   for (int r : never) new_order.push_back(r);
   for (int r : unbounded) new_order.push_back(r);  // the last n_unbounded, tested by every ray
   sc.n_unbounded = (int)unbounded.size();
@@ -381,7 +629,7 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
         const Node2& c = B.nodes[kids[k]];
         cb[nk++] = c.box;
         if (c.left < 0) {
-          // leaf entry: 0x80000000 | first primitive << 7 | count (new order == bounded order)
+          // leaf entry: 0x80000000 | first primitive << 7 | count (new order == leaf_refs order)
           out.child[k] = (int32_t)(0x80000000u | ((uint32_t)c.start << 7) | (uint32_t)c.count);
           meta |= (0x80u | (uint32_t)c.count) << (8 * k);
         } else {
@@ -398,9 +646,11 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
   }
 
   // reorder primitive records; keep (reference index, reference leaf) per primitive
-  std::vector<rt_prim> prims(n);
-  sc.prim_refs.assign(n, rt_prim_ref{});
-  for (int i = 0; i < n; ++i) {
+  const int n_out = (int)new_order.size();
+  if (n_out >= (1 << 24)) throw std::runtime_error("BVH: 2^24 or more primitive references");
+  std::vector<rt_prim> prims(n_out);
+  sc.prim_refs.assign(n_out, rt_prim_ref{});
+  for (int i = 0; i < n_out; ++i) {
     int r = new_order[i];
     prims[i] = sc.prims[r];
     sc.prim_refs[i].ref_index = r;

@@ -574,8 +574,9 @@ void build_bvh(Scene& sc) {
   build_wide(sc, boxes, ref_leaf_of);
   {
     const size_t fl = (size_t)sc.prim_stride / 4;
-    sc.prim_blob.assign((size_t)n * fl, 0.0f);
-    for (int k = 0; k < n; ++k) std::memcpy(&sc.prim_blob[(size_t)k * fl], &sc.prims[k], (size_t)sc.prim_stride);
+    const size_t np = sc.prims.size();  // spatial splits may duplicate primitives
+    sc.prim_blob.assign(np * fl, 0.0f);
+    for (size_t k = 0; k < np; ++k) std::memcpy(&sc.prim_blob[(size_t)k * fl], &sc.prims[k], (size_t)sc.prim_stride);
   }
   sc.flags = flags;
 

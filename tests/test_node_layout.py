@@ -6,7 +6,8 @@ unchecked, and its culling is only exact if every box is conservative:
   * the leaf ranges (child[k], n) cover every bounded primitive exactly once (except planes
     that accept no point, kept only for indexing);
   * every Plane primitive's corners lie inside the dequantised grid box of every ancestor slot
-    on its path (origin + q * 2^(e - 127), evaluated in double).
+    on the path of one of its parts (origin + q * 2^(e - 127), evaluated in double); spatial
+    splits store a primitive once per part.
 rt_scene_create repeats the structural part as its input validation.
 """
 import ctypes
@@ -26,7 +27,8 @@ def _arrays(sc):
     nodes = np.frombuffer(ctypes.string_at(d.nodes, d.n_nodes * 64), dtype=NODE) if d.n_nodes else None
     prims = np.frombuffer(ctypes.string_at(d.prims, d.n_prims * d.prim_stride), dtype="<f4").reshape(
         d.n_prims, d.prim_stride // 4)
-    return d, nodes, prims
+    refs = np.frombuffer(ctypes.string_at(d.prim_refs, d.n_prims * 8), dtype="<i4").reshape(d.n_prims, 2)
+    return d, nodes, prims, refs
 
 
 def _slot_box(nd, k):
@@ -39,7 +41,7 @@ def _slot_box(nd, k):
 
 
 def check_tree(sc):
-    d, nodes, prims = _arrays(sc)
+    d, nodes, prims, refs = _arrays(sc)
     n_bounded = d.n_prims - d.n_unbounded
     if d.n_nodes == 0:
         assert n_bounded == 0
@@ -49,6 +51,9 @@ def check_tree(sc):
     is_plane = (prims[:, 15].view(np.uint32) & 3) == 3
     corners = prims[:, [0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14]].reshape(-1, 4, 3).astype(np.float64)
     checked = 0
+    # spatial splits: a primitive may sit in several leaves (parts); every corner of a plane
+    # must lie inside all ancestor boxes of at least one of its parts
+    corner_ok = {}
     stack = [(0, [])]  # (node, ancestor boxes)
     while stack:
         i, boxes = stack.pop()
@@ -75,9 +80,14 @@ def check_tree(sc):
                 for p in range(c, c + n):
                     if not is_plane[p]:
                         continue
+                    inside = np.ones(4, bool)
                     for lo, hi in boxes + [box]:
-                        assert (corners[p] >= lo).all() and (corners[p] <= hi).all(), (i, k, p)
+                        inside &= ((corners[p] >= lo) & (corners[p] <= hi)).all(axis=1)
+                    r = int(refs[p, 0])
+                    corner_ok[r] = corner_ok.get(r, np.zeros(4, bool)) | inside
                     checked += 1
+    for r, ok in corner_ok.items():
+        assert ok.all(), (r, ok)
     assert parents[0] == 0 and (parents[1:] == 1).all()
     # uncovered bounded slots may only be planes that accept no point (kept for indexing)
     assert (covered <= 1).all() and (covered[n_bounded:] == 0).all()
