@@ -1432,14 +1432,15 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const long long n_units = (long long)n_pixels * n_samples;
   if (n_units > 0x7ffffff0LL) return fail(RT_EINVAL, "rt_render_tiles: too many samples in one call (split the tiles)");
   // whole blocks of slots; a wave renders 64 consecutive samples per batch
-  // Slots in flight, sized to this call's samples (measured, 1024^2 x 100 spp soup): the whole
-  // frame (105M samples) runs best with 16M, one rank's share of a 2-way split (52M) with 13M,
-  // of a 4- or 8-way split (26M / 13M) with 6.5M.  Too few slots and each persistent trace wave
-  // sees few fetches (launch tails dominate); too many and the logic step pays for idle slots.
-  long long slot_cap = n_units < (20LL << 20) ? n_units / 2 : n_units / 4;
-  slot_cap = std::max(1LL << 20, std::min(1LL << 24, slot_cap));
-  if (const char* e = std::getenv("RT_SLOTS")) slot_cap = std::max(1LL << 12, std::atoll(e));
-  const int n_slots = (int)(((std::min<long long>(n_units, slot_cap) + kBlock - 1) / kBlock) * kBlock);
+  // Slots in flight: every sample of the call up to 16M (measured with the refill trace kernel,
+  // 1024^2 x 100 spp soup: the whole frame (105M samples) 16M = 26M > 33M; one rank's share of
+  // an 8-way split (13M) all in flight 3370 vs 6.5M 3081 vs 3.3M 2742 Mrays/s; 4-way (26M) 16M
+  // 3726 vs 6.5M 3552; 2-way (52M) 16M 4048 vs 13M 3944).  Fewer slots means more, shorter
+  // steps, each ending in a launch tail; more than 16M only adds idle slots to every logic step.
+  const long long slot_cap = std::min(n_units, 1LL << 24);
+  long long slots = slot_cap;
+  if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
+  const int n_slots = (int)(((std::min<long long>(n_units, slots) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     s->d_tiles = nullptr;
