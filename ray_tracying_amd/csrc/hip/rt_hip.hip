@@ -1141,7 +1141,8 @@ __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slo
                                                       float* query, unsigned int* wave_done) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
   if (slot >= n_slots) return;
-  for (int f = 0; f < F_COUNT; ++f) state[f * n_slots + slot] = 0u;
+  // only the control words: every other field is written by the logic step before it is read
+  // (slots are reused sample after sample without clearing, so nothing may rely on zeros)
   state[F_UNIT * n_slots + slot] = (uint32_t)-2;  // idle: the first logic step pulls a batch
   if ((slot & 63) == 0) wave_done[slot >> 6] = 0u;
   state[F_CTRL * n_slots + slot] = ST_SAMPLE;
