@@ -1097,9 +1097,22 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
   const int ns = a.spp_sqrt <= 1 ? 1 : a.n_samples;
   for (int s0 = 0; s0 < ns; s0 += kRedChunk) {
     const int cw = min(kRedChunk, ns - s0) * 3;  // floats per pixel in this pass
-    for (int i = (int)threadIdx.x; i < np * cw; i += kBlock) {
-      const int j = i / cw, r = i - j * cw;
-      stage[j * kRedStride + r] = base[(size_t)j * row + (size_t)s0 * 3 + r];
+    if ((row & 3) == 0 && (cw & 3) == 0) {  // 16-B aligned rows and chunks: float4 loads
+      const int cw4 = cw >> 2;
+      for (int i = (int)threadIdx.x; i < np * cw4; i += kBlock) {
+        const int j = i / cw4, r = (i - j * cw4) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(base + (size_t)j * row + (size_t)s0 * 3 + r);
+        float* d = stage + j * kRedStride + r;
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+      }
+    } else {
+      for (int i = (int)threadIdx.x; i < np * cw; i += kBlock) {
+        const int j = i / cw, r = i - j * cw;
+        stage[j * kRedStride + r] = base[(size_t)j * row + (size_t)s0 * 3 + r];
+      }
     }
     __syncthreads();
     if ((int)threadIdx.x < np) {
