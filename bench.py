@@ -37,7 +37,7 @@ METRIC = "Mrays/sec (primary+secondary), 1024x1024 @100spp; % HBM roofline"
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate over 8 XCDs
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 NODE_BYTES, PRIM_BYTES = 32, 64  # BASELINE.md / SURVEY.md 8(d) algorithmic bytes
-PMC_PROFILE = "r01_v16"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r01_v17"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
