@@ -8,16 +8,24 @@ soup (planes with c3 == c0, splitmix64 seed 20251226), 1024x1024, -s 10 (100 jit
 refraction + shadow rays), counted by the kernels.  One step = one full frame.
 
 N GPUs: one process per GPU (torch.distributed, RCCL); the frame's 64x64 tiles are dealt
-round-robin to the ranks (image-tile data parallelism, fixed total work -> "strong"
+to the ranks on a 2-D lattice (tiles.tile_rank; image-tile data parallelism, fixed total work -> "strong"
 scaling), each rank renders its tiles into a device buffer and rank 0 gathers the packed
 tiles over RCCL/xGMI inside the timed step.  value = all ranks' rays / max-over-ranks time.
 
-roofline: per-ray algorithmic bytes (32 B per AABB test + 64 B per primitive test, counted
-by an instrumented run of the same frame) x rays per trace launch / the trace kernel's
-average launch duration (HIP events on the launch stream, summed over the timed steps).
+roofline: the traversal kernel (trace_refill_kernel) is bound by
+VALU issue, not by bytes -- the tree and primitives (~0.1 GB) stay on-die -- so the line
+reports it against the VALU peak: useful lane-operations per second (wave64 VALU
+instructions x 64 x lane utilisation, from the committed rocprofv3 PMC pass of the same
+build) over 256 CUs x 2 wave64 instructions per CU-cycle (SIMD-32: one wave64 VALU
+instruction every 2 cycles per SIMD) x 2.4 GHz.  Beside it, per average trace launch (HIP
+events on the launch stream over the timed steps): `hbm` = PMC HBM bytes (traffic) / launch
+time vs 8 TB/s, and `l2` = algorithmic bytes (64 B per BVH4 node visit + 64 B per primitive
+test, counted by an instrumented run of the same frame) / launch time vs the L2's 34.5 TB/s.
+Scenes of a few primitives (C1-C4) get no roofline claim.
 cpu_baseline: the compiled reference (oracle/_ref/ref_driver; kind "reference") -- or the
 oracle restatement if the reference binary is absent (kind "port") -- on rank 0 at N=1,
-single-threaded, on a bounded row band of the same frame.
+single-threaded, on a bounded row band of the same frame; plus the same band size run as
+concurrent single-threaded processes, one per usable host core (at most 16).
 """
 from __future__ import annotations
 
@@ -36,12 +44,24 @@ sys.path.insert(0, ROOT)
 METRIC = "Mrays/sec (primary+secondary), 1024x1024 @100spp; % HBM roofline"
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate over 8 XCDs
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-NODE_BYTES, PRIM_BYTES = 32, 64  # BASELINE.md / SURVEY.md 8(d) algorithmic bytes
-PMC_PROFILE = "r01_v17"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+# VALU peak (MI355X_MICROARCH.md "Execution model"): 256 CUs x 4 SIMD-32, a wave64 VALU
+# instruction every 2 cycles per SIMD -> 2 wave64 instructions = 128 lane-ops per CU-cycle
+N_CU, VALU_WAVE_INSTR_PER_CU_CYCLE, MAX_CLOCK_GHZ = 256, 2, 2.4
+VALU_PEAK_TOPS = N_CU * VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3  # 78.6 T lane-ops/s
+NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
+PMC_PROFILE = "r02_v1"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def usable_cpus() -> int:
+    """Cores this process may run on (the job's CPU share; os.cpu_count() is the whole host)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
 def parse():
@@ -65,8 +85,9 @@ def parse():
                     help="override every light's radius (SURVEY.md 8(d) C4: soft shadows, e.g. 1.0)")
     ap.add_argument("--primary-only", action="store_true",
                     help="SURVEY.md 8(d) C2 BVH-stress variant: the soup without lights (one ray per sample)")
-    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
-                    help="concurrent reference processes for the all-cores CPU figure (<= 1: skip)")
+    ap.add_argument("--cpu-procs", type=int, default=min(16, usable_cpus()),
+                    help="concurrent reference processes for the multi-core CPU figure (<= 1: skip); default: "
+                         "one per usable host core, at most 16")
     ap.add_argument("--pmc-traffic", default=None,
                     help="JSON with per-launch HBM bytes of the trace kernel (tools/pmc_traffic.py); default: the "
                          "committed profile of the headline workload, attached to that workload only")
@@ -135,10 +156,11 @@ def cpu_baseline(scene_path: str, args, rank: int):
             stk = json.loads(so.strip().splitlines()[-1])
             rates.append(stk["rays"] / stk["render_seconds"] / 1e6)
             total += stk["rays"]
-        out["value_all_cores"] = sum(rates)
-        out["cores_all"] = n
-        out["sample_all_cores"] = (f"{n} concurrent single-threaded processes, {band} rows each "
-                                   f"({total} rays); value = sum of the per-process render rates")
+        out["value_multi_proc"] = sum(rates)
+        out["procs"] = n
+        out["host_cpus"] = {"usable": usable_cpus(), "os_cpu_count": os.cpu_count()}
+        out["sample_multi_proc"] = (f"{n} concurrent single-threaded processes (one per usable host core, at most "
+                                    f"16), {band} rows each ({total} rays); value = sum of the per-process rates")
     return out
 
 
@@ -223,9 +245,12 @@ def main():
     cp = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=args.seed,
                          count_work=True)
     cst = ds.render_tiles(mine, T, T, out.data_ptr(), cp)
-    bytes_per_ray = (NODE_BYTES * cst.box_tests + PRIM_BYTES * cst.prim_tests) / max(cst.rays, 1)
-    log(f"[rank {rank}] instrumented: rays {cst.rays}, box tests {cst.box_tests} ({cst.box_tests / max(cst.rays, 1):.1f}/ray),"
-        f" prim tests {cst.prim_tests} ({cst.prim_tests / max(cst.rays, 1):.1f}/ray), {bytes_per_ray:.0f} B/ray")
+    prim_bytes = scene.info.prim_stride  # 64 B planes / 128 B transformed records
+    bytes_per_ray = (NODE_BYTES * cst.node_visits + prim_bytes * cst.prim_tests) / max(cst.rays, 1)
+    log(f"[rank {rank}] instrumented: rays {cst.rays}, node visits {cst.node_visits} "
+        f"({cst.node_visits / max(cst.rays, 1):.2f}/ray), box tests {cst.box_tests} "
+        f"({cst.box_tests / max(cst.rays, 1):.1f}/ray), prim tests {cst.prim_tests} "
+        f"({cst.prim_tests / max(cst.rays, 1):.2f}/ray), {bytes_per_ray:.0f} B/ray")
 
     for w in range(args.warmup):
         step(args.seed + 1000 + w)
@@ -273,31 +298,61 @@ def main():
         return
 
     value = rays_all / elapsed / 1e6
-    # average trace-kernel launch: bytes it moves algorithmically / its duration (per-rank
-    # launches run concurrently on different GPUs, so average per launch, then x1 GPU)
+    # average trace-kernel launch (per-rank launches run concurrently on different GPUs, so
+    # average per launch = one GPU's kernel)
     avg_launch_ms = trace_ms_all / max(launches_all, 1)
     avg_launch_bytes = alg_bytes_all / max(launches_all, 1)
-    achieved = avg_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
-    # HBM bytes per trace launch measured by rocprofv3 PMC passes of this same bench
-    # (tools/pmc_traffic.py; FETCH_SIZE x2 + WRITE_SIZE); committed with the kernel version
-    # it was measured on (`label`)
-    # it was measured on (`label`).  The committed profiles describe the headline workload
-    # only, so they are never attached to another scene's line.
+    alg_rate = avg_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
+    # PMC summaries of the headline workload measured by rocprofv3 on this build
+    # (tools/pmc_traffic.py, tools/pmc_valu.py; label = the build they were measured on).
+    # They describe the headline frame only, so they are never attached to another line.
     headline = (args.scene is None and not args.primary_only and args.tris == 1_000_000 and args.res == 1024
                 and args.spp_sqrt == 10 and args.light_samples == 1 and args.emulate <= 1 and world == 1)
     prof = os.path.join(ROOT, "profiles", PMC_PROFILE)
     pmc_traffic = args.pmc_traffic or (prof + "_pmc_traffic.json" if headline else None)
     pmc_valu = args.pmc_valu or (prof + "_pmc_valu.json" if headline else None)
-    traffic, traffic_src, valu = None, None, None
+    traffic, traffic_src, pv = None, None, None
     if pmc_traffic and os.path.exists(pmc_traffic):
         pm = json.load(open(pmc_traffic))
         traffic = pm.get("hbm_bytes_per_launch")
         traffic_src = f"{os.path.relpath(pmc_traffic, ROOT)} ({pm.get('label', '')})"
     if pmc_valu and os.path.exists(pmc_valu):
         pv = json.load(open(pmc_valu))
-        valu = {"issue_frac": pv["valu_issue_frac"], "lane_utilisation": pv["lane_utilisation"],
-                "peak": "one wave64 VALU instruction per CU-cycle", "source": f"{os.path.relpath(pmc_valu, ROOT)} "
-                                                                             f"({pv.get('label', '')})"}
+    kernel = {
+        "kernel": "trace_refill_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
+        "launches_per_step": int(launches_all / args.steps),
+        "trace_share_of_step": round(trace_ms_all / world / (elapsed * 1e3), 3),
+    }
+    if args.scene:  # C1-C4: a few primitives, LDS/L1-resident -- no roofline claim
+        roofline = {"bound": None, "frac": None, "achieved": None, "peak": None, "unit": None, "traffic": None,
+                    "note": "scene of a few primitives (on-die): no roofline claim (SURVEY.md 8(d))", **kernel}
+    else:
+        valu = None
+        if pv:
+            # useful lane-ops/s = wave64 VALU instructions/s x 64 x lane utilisation
+            achieved = pv["valu_g_wave_instr_per_s"] * 64 * pv["lane_utilisation"] / 1e3
+            valu = {"achieved": round(achieved, 3), "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                    "issue_frac": round(pv["valu_g_wave_instr_per_s"] / (N_CU * VALU_WAVE_INSTR_PER_CU_CYCLE *
+                                                                        MAX_CLOCK_GHZ), 4),
+                    "lane_utilisation": pv["lane_utilisation"], "measured_clock_ghz": pv.get("clock_ghz"),
+                    "source": f"{os.path.relpath(pmc_valu, ROOT)} ({pv.get('label', '')})"}
+        hbm_rate = traffic / (avg_launch_ms * 1e-3) / 1e9 if traffic else None
+        roofline = {
+            "bound": "valu",
+            "achieved": valu["achieved"] if valu else None, "peak": round(VALU_PEAK_TOPS, 2),
+            "unit": "T VALU lane-ops/s", "frac": valu["frac"] if valu else None,
+            "traffic": traffic, "traffic_unit": "HBM bytes per trace launch (PMC)", "traffic_source": traffic_src,
+            "peak_definition": "256 CUs x 2 wave64 VALU instructions per CU-cycle (4 SIMD-32) x 64 lanes x 2.4 GHz; "
+                               "achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation",
+            "valu": valu,
+            "hbm": {"achieved_gbs": round(hbm_rate, 1) if hbm_rate else None, "peak_gbs": HBM_PEAK_GBS,
+                    "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None},
+            "l2": {"alg_bytes_per_launch": int(avg_launch_bytes), "alg_bytes_per_ray": round(bytes_per_ray, 1),
+                   "model": "64 B per BVH4 node visit + prim_stride B per primitive test",
+                   "achieved_gbs": round(alg_rate, 1), "peak_gbs": L2_PEAK_GBS,
+                   "frac": round(alg_rate / L2_PEAK_GBS, 4)},
+            **kernel,
+        }
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(scene_path, args, rank)
@@ -313,7 +368,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic",
+        "data": ("reference scene " + os.path.basename(args.scene) if args.scene
+                 else "synthetic (generated triangle soup)"),
         "config": {
             "workload": workload,
             "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample {args.light_samples}",
@@ -321,21 +377,7 @@ def main():
             "rng": "counter (splitmix64 per pixel/sample)",
             **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),
         },
-        "roofline": {
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_unit": "HBM bytes per trace launch", "traffic_source": traffic_src,
-            "alg_bytes_per_launch": int(avg_launch_bytes),
-            "kernel": "trace_refill_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
-            "alg_bytes_per_ray": round(bytes_per_ray, 1), "launches_per_step": int(launches_all / args.steps),
-            "trace_share_of_step": round(trace_ms_all / world / (elapsed * 1e3), 3),
-            # the tree + primitives (~0.1 GB) stay on-die: algorithmic bytes are served by L2 /
-            # Infinity Cache, so frac (vs HBM) can pass 1; the on-die ceiling is the L2's
-            "l2_peak": L2_PEAK_GBS, "frac_of_l2": round(achieved / L2_PEAK_GBS, 4),
-            "hbm_rate": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
-            # what actually binds the traversal: VALU issue (PMC pass)
-            "valu": valu,
-        },
+        "roofline": roofline,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

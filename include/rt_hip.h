@@ -178,6 +178,7 @@ typedef struct rt_stats {
   double trace_ms;     /* HIP-event time summed over the trace_kernel launches only */
   int32_t iterations;  /* logic->trace steps (== trace_kernel launches) */
   int32_t pad;
+  uint64_t node_visits; /* count_work only: BVH4 node visits (one 64-B node fetch each) */
 } rt_stats;
 
 typedef struct rt_scene_s* rt_scene_t;

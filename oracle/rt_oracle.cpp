@@ -27,6 +27,8 @@
 #include <algorithm>
 #include <chrono>
 #include <array>
+#include <atomic>
+#include <thread>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -394,11 +396,14 @@ struct Node {
   std::vector<Shape*> objects;
 };
 
+// The reference's BVH keeps mutable scratch (acceleration.hpp:28 temp_hit_vec); here it is
+// per thread, so oracle_render_regions can run rows on several threads (counter RNG only).
+static thread_local Stats* tl_stats = nullptr;
+static thread_local std::vector<Hit> tl_tmp;
+
 struct BVH {
   std::vector<Shape*> list;
   Node root;
-  Stats* st = nullptr;
-  std::vector<Hit> tmp;
   explicit BVH(const std::vector<Shape*>& shapes) : list(shapes) {  // acceleration.cpp:7-18
     if (!list.empty()) build(0, (int)list.size(), root);
     for (size_t i = 0; i < list.size(); ++i) list[i]->order = (int)i;
@@ -426,6 +431,7 @@ struct BVH {
     build(mid, e, *n.right);
   }
   void helper(const Ray& r, Node& n) {  // acceleration.cpp:67-100
+    Stats* st = tl_stats;
     if (st) st->box_tests++;
     if (!n.box.intersect(r)) return;
     if (n.left || n.right) {
@@ -435,11 +441,12 @@ struct BVH {
       for (Shape* s : n.objects) {
         Hit h;
         if (st) st->prim_tests++;
-        if (s->intersect(h, r)) tmp.push_back(h);
+        if (s->intersect(h, r)) tl_tmp.push_back(h);
       }
     }
   }
   Hit intersect_tree(const Ray& r) {  // acceleration.cpp:103-118
+    std::vector<Hit>& tmp = tl_tmp;
     helper(r, root);
     if (tmp.empty()) {
       Hit miss;
@@ -458,13 +465,13 @@ struct BVH {
     best.shape = nullptr;
     for (Shape* s : list) {
       Hit h;
-      if (st) st->prim_tests++;
+      if (tl_stats) tl_stats->prim_tests++;
       if (s->intersect(h, r) && h.t < best.t) best = h;
     }
     return best;
   }
   Hit get(const Ray& r, bool use_bvh) {  // acceleration.cpp:142-150
-    if (st) st->rays++;
+    if (tl_stats) tl_stats->rays++;
     return use_bvh ? intersect_tree(r) : intersect_linear(r);
   }
 };
@@ -940,7 +947,7 @@ int oracle_render(const char* scene_path, const char* texture_root, const oracle
     if (W <= 0 || H <= 0) return -2;
     if (p->rng_mode == orc::RNG_MT19937 && (x0 != 0 || y0 != 0 || w != W || h != H)) return -3;
     orc::Stats stats;
-    sc.bvh->st = &stats;
+    orc::tl_stats = &stats;
     orc::Rng rng((orc::RngMode)p->rng_mode, p->seed);
     orc::Ctx cx{&sc, p->use_bvh != 0, p->light_samples, &rng};
     for (int y = y0; y < y0 + h; ++y) {
@@ -952,8 +959,71 @@ int oracle_render(const char* scene_path, const char* texture_root, const oracle
       }
     }
     auto t2 = std::chrono::steady_clock::now();
+    orc::tl_stats = nullptr;
     if (st) {
       st->rays = stats.rays; st->box_tests = stats.box_tests; st->prim_tests = stats.prim_tests;
+      st->width = W; st->height = H; st->n_shapes = (int)sc.shapes.size(); st->n_lights = (int)sc.lights.size();
+      st->load_seconds = std::chrono::duration<double>(t1 - t0).count();
+      st->render_seconds = std::chrono::duration<double>(t2 - t1).count();
+    }
+    return 0;
+  } catch (std::exception& e) {
+    std::cerr << "oracle: " << e.what() << std::endl;
+    return -1;
+  }
+}
+
+// Counter-RNG render of several regions of one frame after a single scene load, rows shared
+// by n_threads threads (each pixel's stream is keyed by (seed, pixel, sample), so the split
+// cannot change a value).  regions = n_regions x {x0, y0, w, h}; out_rgb holds the regions
+// back to back, each row-major.  Used by the large-scene GPU parity tests (1M triangles:
+// one load, many tiles).  Returns 0 on success.
+int oracle_render_regions(const char* scene_path, const char* texture_root, const oracle_params* p,
+                          int n_regions, const int* regions, float* out_rgb, oracle_stats* st, int n_threads) {
+  try {
+    if (p->rng_mode != orc::RNG_COUNTER) return -3;
+    auto t0 = std::chrono::steady_clock::now();
+    orc::Scene sc;
+    if (texture_root) sc.texture_root = texture_root;
+    orc::load_scene(scene_path, sc, p->res_w, p->res_h);
+    auto t1 = std::chrono::steady_clock::now();
+    const int W = sc.cam.resx, H = sc.cam.resy;
+    if (W <= 0 || H <= 0) return -2;
+    struct Row { int region, y; size_t off; };
+    std::vector<Row> rows;
+    size_t off = 0;
+    for (int r = 0; r < n_regions; ++r) {
+      const int* g = regions + 4 * r;
+      if (g[0] < 0 || g[1] < 0 || g[2] <= 0 || g[3] <= 0 || g[0] + g[2] > W || g[1] + g[3] > H) return -4;
+      for (int y = 0; y < g[3]; ++y) rows.push_back({r, g[1] + y, off + (size_t)y * g[2] * 3});
+      off += (size_t)g[2] * g[3] * 3;
+    }
+    std::atomic<size_t> next{0};
+    int nt = std::max(1, n_threads);
+    std::vector<orc::Stats> stats(nt);
+    auto work = [&](int t) {
+      orc::tl_stats = &stats[t];
+      orc::Rng rng(orc::RNG_COUNTER, p->seed);
+      orc::Ctx cx{&sc, p->use_bvh != 0, p->light_samples, &rng};
+      for (size_t k; (k = next.fetch_add(1)) < rows.size();) {
+        const Row& row = rows[k];
+        const int* g = regions + 4 * row.region;
+        for (int x = g[0]; x < g[0] + g[2]; ++x) {
+          orc::Color c = orc::pixel_color(x, row.y, p->spp_sqrt, cx);
+          float* o = out_rgb + row.off + (size_t)(x - g[0]) * 3;
+          o[0] = c.r; o[1] = c.g; o[2] = c.b;
+        }
+      }
+      orc::tl_stats = nullptr;
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& t : th) t.join();
+    auto t2 = std::chrono::steady_clock::now();
+    if (st) {
+      *st = oracle_stats{};
+      for (auto& s : stats) { st->rays += s.rays; st->box_tests += s.box_tests; st->prim_tests += s.prim_tests; }
       st->width = W; st->height = H; st->n_shapes = (int)sc.shapes.size(); st->n_lights = (int)sc.lights.size();
       st->load_seconds = std::chrono::duration<double>(t1 - t0).count();
       st->render_seconds = std::chrono::duration<double>(t2 - t1).count();

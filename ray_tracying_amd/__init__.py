@@ -75,7 +75,7 @@ class rt_stats(ctypes.Structure):
     _fields_ = [
         ("rays", ctypes.c_uint64), ("box_tests", ctypes.c_uint64), ("prim_tests", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
-        ("iterations", ctypes.c_int32), ("pad", ctypes.c_int32),
+        ("iterations", ctypes.c_int32), ("pad", ctypes.c_int32), ("node_visits", ctypes.c_uint64),
     ]
 
 
@@ -211,11 +211,12 @@ class RenderStats:
     kernel_ms: float
     trace_ms: float
     iterations: int
+    node_visits: int = 0
 
     @staticmethod
     def of(st: rt_stats) -> "RenderStats":
         return RenderStats(int(st.rays), int(st.box_tests), int(st.prim_tests), float(st.kernel_ms),
-                           float(st.trace_ms), int(st.iterations))
+                           float(st.trace_ms), int(st.iterations), int(st.node_visits))
 
 
 class Scene:

@@ -1530,7 +1530,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.any_query = s->d_fetch + (size_t)fetch_shards_env() * kFetchStride;  // the line after the fetch counters
   la.wave_done = s->d_wave_done;
   la.batch_ctr = s->d_batch_ctr;
-  la.batch_shards = batch_shards_env();
+  // every shard needs a slot-wave to drain it (wave w claims from shard w % batch_shards)
+  la.batch_shards = std::max(1, std::min(batch_shards_env(), n_slots / 64));
   HIP_TRY(hipMemsetAsync(s->d_batch_ctr, 0, (size_t)la.batch_shards * kCtrStride * 4, stream), RT_EDEVICE);
 
   TraceArgs ta{};
@@ -1660,6 +1661,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     stats->kernel_ms = ms;
     stats->trace_ms = trace_ms;
     stats->iterations = iters;
+    stats->node_visits = 0;
+    if (p->count_work) {  // lane-level node visits (trace_counters_out, ctl byte 488)
+      unsigned long long nv = 0;
+      HIP_TRY(hipMemcpy(&nv, ctl + 122, sizeof(nv), hipMemcpyDeviceToHost), RT_EDEVICE);
+      stats->node_visits = nv;
+    }
     if (p->count_work && std::getenv("RT_DIAG")) {
       unsigned long long dg[2] = {0, 0};
       HIP_TRY(hipMemcpy(dg, ctl + 128, sizeof(dg), hipMemcpyDeviceToHost), RT_EDEVICE);

@@ -16,12 +16,14 @@
 //   * Sphere / Cube / Rectangle: the reference's own bbox (swept over time for moving spheres)
 //     + rounding margin.  Non-finite boxes (zero scale) -> unbounded list.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <utility>
 #include <stdexcept>
+#include <thread>
 #include <vector>
 
 #include "scene.hpp"
@@ -100,19 +102,57 @@ static int clip_plane(const double (*in)[3], int n, double (*out)[3], int axis, 
   return m;
 }
 
+// Output of one (sub)tree build: nodes in DFS pre-order (children after their parent, the
+// left subtree before the right one) and the leaf references in DFS order.  Subtrees built on
+// other threads are appended with their indices shifted, which yields exactly the numbering
+// of a sequential build: the tree does not depend on the thread count.
+struct BuildOut {
+  std::vector<Node2> nodes;
+  std::vector<Ref> leaf_refs;
+  void append(BuildOut&& o) {
+    const int dn = (int)nodes.size(), dl = (int)leaf_refs.size();
+    for (Node2& nd : o.nodes) {
+      if (nd.left >= 0) {
+        nd.left += dn;
+        nd.right += dn;
+      } else {
+        nd.start += dl;
+      }
+      nodes.push_back(nd);
+    }
+    leaf_refs.insert(leaf_refs.end(), o.leaf_refs.begin(), o.leaf_refs.end());
+    std::vector<Node2>().swap(o.nodes);
+    std::vector<Ref>().swap(o.leaf_refs);
+  }
+};
+
+// Run fn(chunk, begin, end) over `n` items in `chunks` contiguous chunks on their own threads.
+template <class F>
+static void parallel_chunks(size_t n, int chunks, F&& fn) {
+  std::vector<std::thread> th;
+  const size_t per = (n + chunks - 1) / chunks;
+  for (int c = 1; c < chunks; ++c) {
+    const size_t b = std::min(n, c * per), e = std::min(n, (c + 1) * per);
+    th.emplace_back([&fn, c, b, e] { fn(c, b, e); });
+  }
+  fn(0, 0, std::min(n, per));
+  for (auto& t : th) t.join();
+}
+
 struct SAHBuilder {
   std::vector<BuildPrim>& P;
   const Polys& polys;
   float pad_abs;  // 1e-5 * scene scale
-  std::vector<Node2> nodes;
-  std::vector<Ref> leaf_refs;
   static constexpr int kBinsMax = 64;
   int kBins = 32;          // RT_SAH_BINS (tuning knob; 16 -> 32 and node 1.0 -> 0.5: +1.2%)
   int kMaxLeaf = 4;        // RT_SAH_LEAF
   float kNodeCost = 0.5f;  // RT_SAH_NODE: traversal step cost relative to one primitive test
   float kSplitAlpha = 1e-5f;  // RT_SBVH_ALPHA: try spatial splits when children overlap > alpha * root area
-  long long dup_budget = 0;   // RT_SBVH_DUP: extra references allowed (fraction of the primitives)
   float root_area = 0.0f;
+  int threads = 1;                    // RT_BUILD_THREADS
+  std::atomic<int> spare{0};          // threads free to take a subtree
+  static constexpr size_t kSpawnMin = 2048;     // smallest subtree handed to another thread
+  static constexpr size_t kChunkMin = 65536;    // nodes this large bin / partition on all threads
 
   Box pad(Box b) const {
     for (int i = 0; i < 3; ++i) {
@@ -182,57 +222,140 @@ struct SAHBuilder {
       if (part[k].lo[0] <= part[k].hi[0]) bb[k].merge(intersect(pad(part[k]), r.box));
   }
 
-  int make_leaf(int id, std::vector<Ref>& refs) {
-    nodes[id].start = (int)leaf_refs.size();
-    nodes[id].count = (int)refs.size();
-    leaf_refs.insert(leaf_refs.end(), refs.begin(), refs.end());
-    return id;
+  static void make_leaf(BuildOut& out, int id, std::vector<Ref>& refs) {
+    out.nodes[id].start = (int)out.leaf_refs.size();
+    out.nodes[id].count = (int)refs.size();
+    out.leaf_refs.insert(out.leaf_refs.end(), refs.begin(), refs.end());
   }
 
-  int build(std::vector<Ref> refs, int depth) {
-    int id = (int)nodes.size();
-    nodes.emplace_back();
+  static float centroid(const Ref& r, int ax) { return 0.5f * (r.box.lo[ax] + r.box.hi[ax]); }
+
+  // Object-split bins of refs[b, e) on all three axes (centroid bins over `cb`).
+  struct ObjBins {
+    Box bb[3][kBinsMax];
+    int cnt[3][kBinsMax] = {};
+  };
+  void object_bins(const std::vector<Ref>& refs, size_t b, size_t e, const Box& cb, ObjBins& o) const {
+    for (int ax = 0; ax < 3; ++ax) {
+      const float lo = cb.lo[ax], hi = cb.hi[ax];
+      if (!(hi > lo)) continue;
+      const float scale = kBins / (hi - lo);
+      for (size_t i = b; i < e; ++i) {
+        const Ref& r = refs[i];
+        const int k = std::min(kBins - 1, (int)((centroid(r, ax) - lo) * scale));
+        o.bb[ax][k].merge(r.box);
+        o.cnt[ax][k]++;
+      }
+    }
+  }
+
+  // Spatial-split bins of refs[b, e) on axis `ax` over the node box: each reference clipped
+  // into every bin it spans (entering / leaving counts as in SBVH).
+  struct SpBins {
+    Box bb[kBinsMax];
+    int enter[kBinsMax] = {}, leave[kBinsMax] = {};
+  };
+  void spatial_bins(const std::vector<Ref>& refs, size_t b, size_t e, int ax, float lo, float w, SpBins& o) const {
+    for (size_t i = b; i < e; ++i) {
+      const Ref& r = refs[i];
+      int b0 = std::min(kBins - 1, std::max(0, (int)((r.box.lo[ax] - lo) / w)));
+      int b1 = std::min(kBins - 1, std::max(0, (int)((r.box.hi[ax] - lo) / w)));
+      if (polys.n[r.p] == 0) b0 = b1 = std::min(kBins - 1, std::max(0, (int)((centroid(r, ax) - lo) / w)));
+      if (b0 == b1)
+        o.bb[b0].merge(r.box);
+      else
+        sweep_bins(r, ax, lo, w, b0, b1, o.bb);
+      o.enter[b0]++;
+      o.leave[b1]++;
+    }
+  }
+
+  // Partition refs[b, e) by the chosen split into L / R (spatial: straddlers clipped into
+  // both sides); returns the number of references duplicated.
+  long long partition(const std::vector<Ref>& refs, size_t b, size_t e, int sp_axis, float sp_pos, int best_axis,
+                      int best_bin, float obj_lo, float obj_scale, std::vector<Ref>& L, std::vector<Ref>& R) const {
+    long long dup = 0;
+    for (size_t i = b; i < e; ++i) {
+      const Ref& r = refs[i];
+      if (sp_axis < 0) {
+        (std::min(kBins - 1, (int)((centroid(r, best_axis) - obj_lo) * obj_scale)) <= best_bin ? L : R).push_back(r);
+        continue;
+      }
+      if (polys.n[r.p] == 0) {
+        (centroid(r, sp_axis) < sp_pos ? L : R).push_back(r);
+        continue;
+      }
+      if (r.box.hi[sp_axis] <= sp_pos) { L.push_back(r); continue; }
+      if (r.box.lo[sp_axis] >= sp_pos) { R.push_back(r); continue; }
+      Box cl = r.clip, cr = r.clip;
+      cl.hi[sp_axis] = std::min(cl.hi[sp_axis], sp_pos);
+      cr.lo[sp_axis] = std::max(cr.lo[sp_axis], sp_pos);
+      Ref a, c;
+      const bool ha = clipped(r, cl, a), hc = clipped(r, cr, c);
+      if (ha) L.push_back(a);
+      if (hc) R.push_back(c);
+      if (ha && hc) ++dup;
+      if (!ha && !hc) L.push_back(r);  // cannot happen for a nonempty polygon; keep it anyway
+    }
+    return dup;
+  }
+
+  // Builds the subtree over `refs` into `out` (its root is out.nodes[returned id]).
+  // `budget` = duplicate references this subtree may still create by spatial splits; it is
+  // shared between the two children in proportion to their sizes, so the tree is the same
+  // for every thread count (and a chosen split never exceeds it: candidates whose straddling
+  // references outnumber the budget are skipped).
+  int build(std::vector<Ref> refs, int depth, long long budget, BuildOut& out) {
+    const int id = (int)out.nodes.size();
+    out.nodes.emplace_back();
     Box b, cb;
     for (const Ref& r : refs) {
       b.merge(r.box);
-      cb.merge(V3{0.5f * (r.box.lo[0] + r.box.hi[0]), 0.5f * (r.box.lo[1] + r.box.hi[1]),
-                  0.5f * (r.box.lo[2] + r.box.hi[2])});
+      cb.merge(V3{centroid(r, 0), centroid(r, 1), centroid(r, 2)});
     }
-    nodes[id].box = b;
+    out.nodes[id].box = b;
     if (depth == 0) root_area = area(b);
     const int n = (int)refs.size();
-    if (n <= 1 || depth > 60) return make_leaf(id, refs);
-    auto centroid = [](const Ref& r, int ax) { return 0.5f * (r.box.lo[ax] + r.box.hi[ax]); };
+    if (n <= 1 || depth > 60) {
+      make_leaf(out, id, refs);
+      return id;
+    }
+    const bool wide = (size_t)n >= kChunkMin && threads > 1;
+    const int chunks = wide ? threads : 1;
     // object split: binned SAH over all three axes
+    ObjBins ob;
+    if (wide) {
+      std::vector<ObjBins> part(chunks);
+      parallel_chunks(refs.size(), chunks, [&](int c, size_t s, size_t e) { object_bins(refs, s, e, cb, part[c]); });
+      for (const ObjBins& p : part)
+        for (int ax = 0; ax < 3; ++ax)
+          for (int k = 0; k < kBins; ++k) {
+            ob.bb[ax][k].merge(p.bb[ax][k]);
+            ob.cnt[ax][k] += p.cnt[ax][k];
+          }
+    } else {
+      object_bins(refs, 0, refs.size(), cb, ob);
+    }
     float best_cost = INFINITY;
     int best_axis = -1, best_bin = -1;
     Box best_l, best_r;
     for (int ax = 0; ax < 3; ++ax) {
-      float lo = cb.lo[ax], hi = cb.hi[ax];
-      if (!(hi > lo)) continue;
-      float scale = kBins / (hi - lo);
-      Box bb[kBinsMax];
-      int cnt[kBinsMax] = {0};
-      for (const Ref& r : refs) {
-        int k = std::min(kBins - 1, (int)((centroid(r, ax) - lo) * scale));
-        bb[k].merge(r.box);
-        cnt[k]++;
-      }
+      if (!(cb.hi[ax] > cb.lo[ax])) continue;
       Box rb[kBinsMax];
       int rc[kBinsMax];
       Box acc;
       int c = 0;
       for (int k = kBins - 1; k > 0; --k) {
-        acc.merge(bb[k]);
-        c += cnt[k];
+        acc.merge(ob.bb[ax][k]);
+        c += ob.cnt[ax][k];
         rb[k] = acc;
         rc[k] = c;
       }
       Box accl;
       int cl = 0;
       for (int k = 0; k < kBins - 1; ++k) {
-        accl.merge(bb[k]);
-        cl += cnt[k];
+        accl.merge(ob.bb[ax][k]);
+        cl += ob.cnt[ax][k];
         if (cl == 0 || rc[k + 1] == 0) continue;
         float cost = area(accl) * cl + area(rb[k + 1]) * rc[k + 1];
         if (cost < best_cost) {
@@ -247,40 +370,42 @@ struct SAHBuilder {
     // spatial split: bins over the node box, references clipped into every bin they span
     int sp_axis = -1;
     float sp_pos = 0.0f;
-    if (dup_budget > 0 && best_axis >= 0 && area(intersect(best_l, best_r)) > kSplitAlpha * root_area) {
+    if (budget > 0 && best_axis >= 0 && area(intersect(best_l, best_r)) > kSplitAlpha * root_area) {
       for (int ax = 0; ax < 3; ++ax) {
         const float lo = b.lo[ax], hi = b.hi[ax];
         if (!(hi > lo)) continue;
         const float w = (hi - lo) / kBins;
-        Box bb[kBinsMax];
-        int enter[kBinsMax] = {0}, leave[kBinsMax] = {0};
-        for (const Ref& r : refs) {
-          int b0 = std::min(kBins - 1, std::max(0, (int)((r.box.lo[ax] - lo) / w)));
-          int b1 = std::min(kBins - 1, std::max(0, (int)((r.box.hi[ax] - lo) / w)));
-          if (polys.n[r.p] == 0) b0 = b1 = std::min(kBins - 1, std::max(0, (int)((centroid(r, ax) - lo) / w)));
-          if (b0 == b1)
-            bb[b0].merge(r.box);
-          else
-            sweep_bins(r, ax, lo, w, b0, b1, bb);
-          enter[b0]++;
-          leave[b1]++;
+        SpBins sb;
+        if (wide) {
+          std::vector<SpBins> part(chunks);
+          parallel_chunks(refs.size(), chunks,
+                          [&](int c, size_t s, size_t e) { spatial_bins(refs, s, e, ax, lo, w, part[c]); });
+          for (const SpBins& p : part)
+            for (int k = 0; k < kBins; ++k) {
+              sb.bb[k].merge(p.bb[k]);
+              sb.enter[k] += p.enter[k];
+              sb.leave[k] += p.leave[k];
+            }
+        } else {
+          spatial_bins(refs, 0, refs.size(), ax, lo, w, sb);
         }
         Box rb[kBinsMax];
         int rc[kBinsMax];
         Box acc;
         int c = 0;
         for (int k = kBins - 1; k > 0; --k) {
-          acc.merge(bb[k]);
-          c += leave[k];
+          acc.merge(sb.bb[k]);
+          c += sb.leave[k];
           rb[k] = acc;
           rc[k] = c;
         }
         Box accl;
         int cl = 0;
         for (int k = 0; k < kBins - 1; ++k) {
-          accl.merge(bb[k]);
-          cl += enter[k];
+          accl.merge(sb.bb[k]);
+          cl += sb.enter[k];
           if (cl == 0 || rc[k + 1] == 0) continue;
+          if ((long long)cl + rc[k + 1] - n > budget) continue;  // straddlers past the budget
           float cost = area(accl) * cl + area(rb[k + 1]) * rc[k + 1];
           if (cost < best_cost) {
             best_cost = cost;
@@ -292,31 +417,36 @@ struct SAHBuilder {
     }
     const float leaf_cost = area(b) * n;
     const float node_cost = area(b) * kNodeCost;  // traversal step relative to one primitive test
-    if (n <= kMaxLeaf && ((best_axis < 0 && sp_axis < 0) || best_cost * 1.0f + node_cost >= leaf_cost))
-      return make_leaf(id, refs);
+    if (n <= kMaxLeaf && ((best_axis < 0 && sp_axis < 0) || best_cost * 1.0f + node_cost >= leaf_cost)) {
+      make_leaf(out, id, refs);
+      return id;
+    }
     std::vector<Ref> L, R;
-    if (sp_axis >= 0) {
-      for (const Ref& r : refs) {
-        const bool poly = polys.n[r.p] != 0;
-        if (!poly) {
-          (centroid(r, sp_axis) < sp_pos ? L : R).push_back(r);
-          continue;
+    long long dup = 0;
+    const float obj_lo = best_axis >= 0 ? cb.lo[best_axis] : 0.0f;
+    const float obj_scale = best_axis >= 0 ? kBins / (cb.hi[best_axis] - obj_lo) : 0.0f;
+    auto split = [&](int axis) {
+      if (wide) {
+        std::vector<std::vector<Ref>> pl(chunks), pr(chunks);
+        std::vector<long long> pd(chunks, 0);
+        parallel_chunks(refs.size(), chunks, [&](int c, size_t s, size_t e) {
+          pd[c] = partition(refs, s, e, axis, sp_pos, best_axis, best_bin, obj_lo, obj_scale, pl[c], pr[c]);
+        });
+        for (int c = 0; c < chunks; ++c) {  // chunk order == sequential order
+          L.insert(L.end(), pl[c].begin(), pl[c].end());
+          R.insert(R.end(), pr[c].begin(), pr[c].end());
+          dup += pd[c];
         }
-        if (r.box.hi[sp_axis] <= sp_pos) { L.push_back(r); continue; }
-        if (r.box.lo[sp_axis] >= sp_pos) { R.push_back(r); continue; }
-        Box cl = r.clip, cr = r.clip;
-        cl.hi[sp_axis] = std::min(cl.hi[sp_axis], sp_pos);
-        cr.lo[sp_axis] = std::max(cr.lo[sp_axis], sp_pos);
-        Ref a, c;
-        const bool ha = clipped(r, cl, a), hc = clipped(r, cr, c);
-        if (ha) L.push_back(a);
-        if (hc) R.push_back(c);
-        if (ha && hc) --dup_budget;
-        if (!ha && !hc) L.push_back(r);  // cannot happen for a nonempty polygon; keep it anyway
+      } else {
+        dup = partition(refs, 0, refs.size(), axis, sp_pos, best_axis, best_bin, obj_lo, obj_scale, L, R);
       }
+    };
+    if (sp_axis >= 0) {
+      split(sp_axis);
       if (L.empty() || R.empty()) {  // degenerate: fall back to the object split below
         L.clear();
         R.clear();
+        dup = 0;
         sp_axis = -1;
       }
     }
@@ -325,9 +455,7 @@ struct SAHBuilder {
         L.assign(refs.begin(), refs.begin() + n / 2);
         R.assign(refs.begin() + n / 2, refs.end());
       } else {
-        float lo = cb.lo[best_axis], scale = kBins / (cb.hi[best_axis] - lo);
-        for (const Ref& r : refs)
-          (std::min(kBins - 1, (int)((centroid(r, best_axis) - lo) * scale)) <= best_bin ? L : R).push_back(r);
+        split(-1);
         if (L.empty() || R.empty()) {
           L.assign(refs.begin(), refs.begin() + n / 2);
           R.assign(refs.begin() + n / 2, refs.end());
@@ -335,14 +463,34 @@ struct SAHBuilder {
       }
     }
     std::vector<Ref>().swap(refs);
-    int l = build(std::move(L), depth + 1);
-    int r = build(std::move(R), depth + 1);
-    nodes[id].left = l;
-    nodes[id].right = r;
-    nodes[id].count = 0;
+    const long long left_budget = std::max(0LL, budget - dup);
+    const long long bl = (long long)((double)left_budget * (double)L.size() / (double)(L.size() + R.size()));
+    const long long br = left_budget - bl;
+    int l, r;
+    int tok = spare.load();
+    const bool spawn = L.size() >= kSpawnMin && R.size() >= kSpawnMin && tok > 0 &&
+                       spare.compare_exchange_strong(tok, tok - 1);
+    if (spawn) {  // left subtree on another thread, right here; appended in DFS order
+      BuildOut lo, ro;
+      std::thread t([&] { build(std::move(L), depth + 1, bl, lo); });
+      build(std::move(R), depth + 1, br, ro);
+      t.join();
+      spare.fetch_add(1);
+      l = (int)out.nodes.size();
+      out.append(std::move(lo));
+      r = (int)out.nodes.size();
+      out.append(std::move(ro));
+    } else {
+      l = build(std::move(L), depth + 1, bl, out);
+      r = build(std::move(R), depth + 1, br, out);
+    }
+    out.nodes[id].left = l;
+    out.nodes[id].right = r;
+    out.nodes[id].count = 0;
     return id;
   }
 };
+
 
 // Accepted region of isPointInTriangle(P, A, B, C, n) (shapes.cpp:24-40) for P in the plane:
 // dot(cross(E_i, P - V_i), n) >= -tol for the three edges (E_1 = B-A at A, E_2 = C-B at B,
@@ -470,6 +618,7 @@ static void quantise_children(rt_node4& out, const Box* cb, int n) {
 // `ref_order` = the reference's BVH-sorted shape order, `ref_leaf_of` = reference leaf id per
 // sorted position, `ref_leaf_boxes` = the exact reference leaf boxes.
 void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<int>& ref_leaf_of) {
+  BuildTimer tm("build_wide");
   const int n = (int)sc.order.size();
   const float margin = 1e-5f * sc.scene_scale;
   std::vector<BuildPrim> bounded;
@@ -479,85 +628,115 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
   std::vector<int> never;      // planes that accept no point: kept for indexing, never traversed
   Polys polys;                 // per bounded primitive: acceptance triangles (spatial splits)
   bounded.reserve(n);
-  for (int r = 0; r < n; ++r) {
-    const Shape& s = sc.shapes[sc.order[r]];
-    Box b = shape_box[sc.order[r]];
-    bool ok = true;
-    float pad = margin;
-    std::vector<double> tv1, tv2;  // the two sub-triangles' acceptance regions (3 vertices each)
-    if (s.kind == RT_PRIM_PLANE) {
-      // isPointInQuad = triangle (c1,c3,c2) OR triangle (c0,c1,c2) (shapes.cpp:485-494); the
-      // acceptance regions (2x the reference's 1e-6 tolerance for float rounding) bound every
-      // hit point.  Invalid planes (|cross| < 1e-6f) never hit and are left out entirely.
-      uint32_t tag;
-      std::memcpy(&tag, &sc.prims[r].a[15], 4);
-      if (!(tag & RT_TAG_PLANE_VALID)) { never.push_back(r); continue; }
-      const V3* c = s.corners;
-      double C[4][3], nn[3];
-      for (int q = 0; q < 4; ++q)
-        for (int m = 0; m < 3; ++m) C[q][m] = c[q][m];
-      double e1[3] = {C[1][0] - C[0][0], C[1][1] - C[0][1], C[1][2] - C[0][2]};
-      double e2[3] = {C[2][0] - C[0][0], C[2][1] - C[0][1], C[2][2] - C[0][2]};
-      nn[0] = e1[1] * e2[2] - e1[2] * e2[1];
-      nn[1] = e1[2] * e2[0] - e1[0] * e2[2];
-      nn[2] = e1[0] * e2[1] - e1[1] * e2[0];
-      double ln = std::sqrt(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
-      for (double& x : nn) x /= ln;
-      Box region;
-      bool ne1 = false, ne2 = false;
-      ok = tri_region(C[1], C[3], C[2], nn, 2e-6, region, ne1, &tv1) &&
-           tri_region(C[0], C[1], C[2], nn, 2e-6, region, ne2, &tv2);
-      if (ok && !ne1 && !ne2) { never.push_back(r); continue; }  // accepts nothing
-      if (ok) {
-        b = region;
-        accept_box[r] = region;
-        has_accept[r] = 1;
+  // per-primitive classification on all build threads (chunks of the sorted positions),
+  // concatenated in chunk order == the sequential order
+  struct Part {
+    std::vector<BuildPrim> bounded;
+    std::vector<int> never, unbounded;
+    Polys polys;
+  };
+  const int nchunks = n >= 65536 ? build_threads() : 1;
+  std::vector<Part> parts(nchunks);
+  parallel_chunks((size_t)n, nchunks, [&](int ci, size_t rb, size_t re) {
+    Part& pt = parts[ci];
+    for (int r = (int)rb; r < (int)re; ++r) {
+      const Shape& s = sc.shapes[sc.order[r]];
+      Box b = shape_box[sc.order[r]];
+      bool ok = true;
+      float pad = margin;
+      std::vector<double> tv1, tv2;  // the two sub-triangles' acceptance regions (3 vertices each)
+      if (s.kind == RT_PRIM_PLANE) {
+        // isPointInQuad = triangle (c1,c3,c2) OR triangle (c0,c1,c2) (shapes.cpp:485-494); the
+        // acceptance regions (2x the reference's 1e-6 tolerance for float rounding) bound every
+        // hit point.  Invalid planes (|cross| < 1e-6f) never hit and are left out entirely.
+        uint32_t tag;
+        std::memcpy(&tag, &sc.prims[r].a[15], 4);
+        if (!(tag & RT_TAG_PLANE_VALID)) { pt.never.push_back(r); continue; }
+        const V3* c = s.corners;
+        double C[4][3], nn[3];
+        for (int q = 0; q < 4; ++q)
+          for (int m = 0; m < 3; ++m) C[q][m] = c[q][m];
+        double e1[3] = {C[1][0] - C[0][0], C[1][1] - C[0][1], C[1][2] - C[0][2]};
+        double e2[3] = {C[2][0] - C[0][0], C[2][1] - C[0][1], C[2][2] - C[0][2]};
+        nn[0] = e1[1] * e2[2] - e1[2] * e2[1];
+        nn[1] = e1[2] * e2[0] - e1[0] * e2[2];
+        nn[2] = e1[0] * e2[1] - e1[1] * e2[0];
+        double ln = std::sqrt(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
+        for (double& x : nn) x /= ln;
+        Box region;
+        bool ne1 = false, ne2 = false;
+        ok = tri_region(C[1], C[3], C[2], nn, 2e-6, region, ne1, &tv1) &&
+             tri_region(C[0], C[1], C[2], nn, 2e-6, region, ne2, &tv2);
+        if (ok && !ne1 && !ne2) { pt.never.push_back(r); continue; }  // accepts nothing
+        if (ok) {
+          b = region;
+          accept_box[r] = region;
+          has_accept[r] = 1;
+        }
       }
-    }
-    for (int i = 0; i < 3; ++i) {
-      b.lo[i] -= pad + std::fabs(b.lo[i]) * 2e-6f;
-      b.hi[i] += pad + std::fabs(b.hi[i]) * 2e-6f;
-      if (!std::isfinite(b.lo[i]) || !std::isfinite(b.hi[i])) ok = false;
-    }
-    if (!ok) {
-      unbounded.push_back(r);
-      continue;
-    }
-    // polygons only when both regions are whole triangles or empty (otherwise: never split)
-    int ntri = 0;
-    if ((tv1.size() == 9 || tv1.empty()) && (tv2.size() == 9 || tv2.empty()) && !(tv1.empty() && tv2.empty())) {
-      // c3 == c0 makes both sub-triangles the same triangle: keep one copy
-      bool same = tv1.size() == 9 && tv2.size() == 9;
-      for (int k = 0; k < 3 && same; ++k) {
-        bool found = false;
-        for (int m = 0; m < 3 && !found; ++m)
-          found = std::fabs(tv1[k * 3] - tv2[m * 3]) + std::fabs(tv1[k * 3 + 1] - tv2[m * 3 + 1]) +
-                      std::fabs(tv1[k * 3 + 2] - tv2[m * 3 + 2]) <= 1e-12 * (1.0 + std::fabs(tv1[k * 3]));
-        same = found;
+      for (int i = 0; i < 3; ++i) {
+        b.lo[i] -= pad + std::fabs(b.lo[i]) * 2e-6f;
+        b.hi[i] += pad + std::fabs(b.hi[i]) * 2e-6f;
+        if (!std::isfinite(b.lo[i]) || !std::isfinite(b.hi[i])) ok = false;
       }
-      polys.off.push_back((int)(polys.v.size() / 9));
-      polys.v.insert(polys.v.end(), tv1.begin(), tv1.end());
-      if (!same) polys.v.insert(polys.v.end(), tv2.begin(), tv2.end());
-      ntri = (int)(polys.v.size() / 9) - polys.off.back();
-    } else {
-      polys.off.push_back((int)(polys.v.size() / 9));
+      if (!ok) {
+        pt.unbounded.push_back(r);
+        continue;
+      }
+      // polygons only when both regions are whole triangles or empty (otherwise: never split)
+      int ntri = 0;
+      if ((tv1.size() == 9 || tv1.empty()) && (tv2.size() == 9 || tv2.empty()) && !(tv1.empty() && tv2.empty())) {
+        // c3 == c0 makes both sub-triangles the same triangle: keep one copy
+        bool same = tv1.size() == 9 && tv2.size() == 9;
+        for (int k = 0; k < 3 && same; ++k) {
+          bool found = false;
+          for (int m = 0; m < 3 && !found; ++m)
+            found = std::fabs(tv1[k * 3] - tv2[m * 3]) + std::fabs(tv1[k * 3 + 1] - tv2[m * 3 + 1]) +
+                        std::fabs(tv1[k * 3 + 2] - tv2[m * 3 + 2]) <= 1e-12 * (1.0 + std::fabs(tv1[k * 3]));
+          same = found;
+        }
+        pt.polys.off.push_back((int)(pt.polys.v.size() / 9));
+        pt.polys.v.insert(pt.polys.v.end(), tv1.begin(), tv1.end());
+        if (!same) pt.polys.v.insert(pt.polys.v.end(), tv2.begin(), tv2.end());
+        ntri = (int)(pt.polys.v.size() / 9) - pt.polys.off.back();
+      } else {
+        pt.polys.off.push_back((int)(pt.polys.v.size() / 9));
+      }
+      pt.polys.n.push_back(ntri);
+      BuildPrim bp;
+      bp.box = b;
+      bp.c = {0.5f * (b.lo[0] + b.hi[0]), 0.5f * (b.lo[1] + b.hi[1]), 0.5f * (b.lo[2] + b.hi[2])};
+      bp.id = r;
+      pt.bounded.push_back(bp);
     }
-    polys.n.push_back(ntri);
-    BuildPrim bp;
-    bp.box = b;
-    bp.c = {0.5f * (b.lo[0] + b.hi[0]), 0.5f * (b.lo[1] + b.hi[1]), 0.5f * (b.lo[2] + b.hi[2])};
-    bp.id = r;
-    bounded.push_back(bp);
+  });
+  for (Part& pt : parts) {
+    const int voff = (int)(polys.v.size() / 9);
+    bounded.insert(bounded.end(), pt.bounded.begin(), pt.bounded.end());
+    never.insert(never.end(), pt.never.begin(), pt.never.end());
+    unbounded.insert(unbounded.end(), pt.unbounded.begin(), pt.unbounded.end());
+    polys.v.insert(polys.v.end(), pt.polys.v.begin(), pt.polys.v.end());
+    for (int o : pt.polys.off) polys.off.push_back(o + voff);
+    polys.n.insert(polys.n.end(), pt.polys.n.begin(), pt.polys.n.end());
+    Part().bounded.swap(pt.bounded);
   }
-  SAHBuilder B{bounded, polys, margin, {}, {}};
+  std::vector<Part>().swap(parts);
+  tm.lap("acceptance regions");
+  SAHBuilder B{bounded, polys, margin};
   if (const char* e = std::getenv("RT_SAH_BINS")) B.kBins = std::max(2, std::min(SAHBuilder::kBinsMax, std::atoi(e)));
   if (const char* e = std::getenv("RT_SAH_LEAF")) B.kMaxLeaf = std::max(1, std::min(15, std::atoi(e)));
   if (const char* e = std::getenv("RT_SAH_NODE")) B.kNodeCost = (float)std::atof(e);
   if (const char* e = std::getenv("RT_SBVH_ALPHA")) B.kSplitAlpha = (float)std::atof(e);
   double dup = kSbvhDup;
   if (const char* e = std::getenv("RT_SBVH_DUP")) dup = std::max(0.0, std::min(4.0, std::atof(e)));
-  B.dup_budget = (long long)(dup * (double)bounded.size());
-  B.nodes.reserve(bounded.size() + 1);
+  B.threads = build_threads();
+  B.spare = B.threads - 1;
+  // duplicates allowed: the RT_SBVH_DUP fraction, and never past the 24-bit leaf packing
+  const long long ref_cap = (1LL << 24) - 1 - (long long)(n - (int)bounded.size());
+  const long long budget = std::max(0LL, std::min((long long)(dup * (double)bounded.size()),
+                                                  ref_cap - (long long)bounded.size()));
+  BuildOut T;
+  T.nodes.reserve(bounded.size() + 1);
   if (!bounded.empty()) {
     std::vector<Ref> refs(bounded.size());
     Box open;  // no clip yet
@@ -566,14 +745,15 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
       open.hi[a] = INFINITY;
     }
     for (size_t i = 0; i < bounded.size(); ++i) refs[i] = Ref{bounded[i].box, open, (int)i};
-    B.build(std::move(refs), 0);
+    B.build(std::move(refs), 0, budget, T);
   }
 
+  tm.lap("SAH/SBVH BVH2");
   // new primitive order: leaf references of the SAH tree (DFS; a primitive split by spatial
   // splits appears once per part), then the never-hit and the unbounded lists
   std::vector<int> new_order;  // new index -> sorted reference position r
-  new_order.reserve(B.leaf_refs.size() + never.size() + unbounded.size());
-  for (const Ref& r : B.leaf_refs) new_order.push_back(bounded[r.p].id);
+  new_order.reserve(T.leaf_refs.size() + never.size() + unbounded.size());
+  for (const Ref& r : T.leaf_refs) new_order.push_back(bounded[r.p].id);
   for (int r : never) new_order.push_back(r);
   for (int r : unbounded) new_order.push_back(r);  // the last n_unbounded, tested by every ray
   sc.n_unbounded = (int)unbounded.size();
@@ -598,7 +778,7 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
       todo.pop_back();
       max_depth = std::max(max_depth, it.depth);
       std::vector<int> kids;
-      const Node2& root = B.nodes[it.n2];
+      const Node2& root = T.nodes[it.n2];
       if (root.left < 0) {
         kids.push_back(it.n2);
       } else {
@@ -607,14 +787,14 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
           int best = -1;
           float ba = -1;
           for (int k = 0; k < (int)kids.size(); ++k) {
-            const Node2& c = B.nodes[kids[k]];
+            const Node2& c = T.nodes[kids[k]];
             if (c.left >= 0 && area(c.box) > ba) { ba = area(c.box); best = k; }
           }
           if (best < 0) break;
           int nb = kids[best];
           kids.erase(kids.begin() + best);
-          kids.push_back(B.nodes[nb].left);
-          kids.push_back(B.nodes[nb].right);
+          kids.push_back(T.nodes[nb].left);
+          kids.push_back(T.nodes[nb].right);
         }
       }
       rt_node4 out{};
@@ -626,7 +806,7 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
           out.child[k] = -1;
           continue;
         }
-        const Node2& c = B.nodes[kids[k]];
+        const Node2& c = T.nodes[kids[k]];
         cb[nk++] = c.box;
         if (c.left < 0) {
           // leaf entry: 0x80000000 | first primitive << 7 | count (new order == leaf_refs order)
@@ -645,6 +825,7 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
     sc.tree_depth = max_depth;
   }
 
+  tm.lap("BVH4 collapse + quantise");
   // reorder primitive records; keep (reference index, reference leaf) per primitive
   const int n_out = (int)new_order.size();
   if (n_out >= (1 << 24)) throw std::runtime_error("BVH: 2^24 or more primitive references");
@@ -674,6 +855,7 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
     }
   }
   sc.prims.swap(prims);
+  tm.lap("reorder + reference-leaf filter");
 }
 
 }  // namespace rth

@@ -96,7 +96,7 @@ int main(int argc, char* argv[]) {
     }
     rays = st.rays;
   } else {
-    // image-tile data parallelism: tile t goes to device (t mod gpus), one host thread per
+    // image-tile data parallelism: tiles dealt on a 2-D lattice (below), one host thread per
     // device renders into a packed device buffer (padded to the largest tile list), then one
     // RCCL gather over xGMI brings every buffer to the first device (include/rt_comm.h)
     rt_scene_desc desc{};

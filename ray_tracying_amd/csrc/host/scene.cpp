@@ -11,14 +11,18 @@
 #include "scene.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
 #include <map>
 #include <sstream>
 #include <stdexcept>
+#include <thread>
 
 #include "json_dom.hpp"
 
@@ -422,6 +426,23 @@ std::unique_ptr<Scene> load_scene(const std::string& path, const std::string& te
 }
 
 // ---------------------------------------------------------------- BVH + flattening
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+BuildTimer::BuildTimer(const char* w) : what(w), on(std::getenv("RT_BUILD_TIMING") != nullptr), t0(now_s()), last(t0) {}
+void BuildTimer::lap(const char* phase) {
+  if (!on) return;
+  const double t = now_s();
+  std::fprintf(stderr, "[%s] %-36s %8.3f s (total %.3f s)\n", what, phase, t - last, t - t0);
+  last = t;
+}
+
+int build_threads() {
+  if (const char* e = std::getenv("RT_BUILD_THREADS")) return std::max(1, std::min(256, std::atoi(e)));
+  const unsigned hc = std::thread::hardware_concurrency();
+  return std::max(1, std::min(16, (int)(hc ? hc : 1)));
+}
+
 namespace {
 
 struct BNode {
@@ -434,10 +455,26 @@ struct BNode {
 struct Builder {
   std::vector<int>& order;
   const std::vector<Box>& boxes;
-  std::vector<BNode> nodes;
   std::vector<float> cent;  // centroid along the current sort axis, per shape
+  std::atomic<int> spare{0};  // threads free to take a subtree
+  static constexpr int kSpawnMin = 16384;
 
-  int build(int start, int end) {  // acceleration.cpp:20-64
+  // Nodes in DFS pre-order (left subtree first).  A subtree built on another thread works on
+  // its own disjoint range of `order` / `cent` and is appended with shifted indices, so the
+  // node numbering (the reference-leaf ids) is the sequential build's for any thread count.
+  static void append(std::vector<BNode>& dst, std::vector<BNode>&& src) {
+    const int d = (int)dst.size();
+    for (BNode& nd : src) {
+      if (nd.left >= 0) {
+        nd.left += d;
+        nd.right += d;
+      }
+      dst.push_back(nd);
+    }
+    std::vector<BNode>().swap(src);
+  }
+
+  int build(int start, int end, std::vector<BNode>& nodes) {  // acceleration.cpp:20-64
     int id = (int)nodes.size();
     nodes.emplace_back();
     Box nb;
@@ -456,8 +493,22 @@ struct Builder {
     // (libstdc++ introsort) produces the same permutation.
     std::sort(order.begin() + start, order.begin() + end, [c](int a, int b) { return c[a] < c[b]; });
     int mid = (start + end) / 2;
-    int l = build(start, mid);
-    int r = build(mid, end);
+    int l, r;
+    int tok = spare.load();
+    if (mid - start >= kSpawnMin && tok > 0 && spare.compare_exchange_strong(tok, tok - 1)) {
+      std::vector<BNode> ln, rn;
+      std::thread t([&] { build(start, mid, ln); });
+      build(mid, end, rn);
+      t.join();
+      spare.fetch_add(1);
+      l = (int)nodes.size();
+      append(nodes, std::move(ln));
+      r = (int)nodes.size();
+      append(nodes, std::move(rn));
+    } else {
+      l = build(start, mid, nodes);
+      r = build(mid, end, nodes);
+    }
     nodes[id].left = l;
     nodes[id].right = r;
     return id;
@@ -472,19 +523,26 @@ float finite_abs_max(float a, float b) {
 }  // namespace
 
 void build_bvh(Scene& sc) {
+  BuildTimer tm("build_bvh");
   const int n = (int)sc.shapes.size();
   std::vector<Box> boxes(n);
   for (int i = 0; i < n; ++i) boxes[i] = sc.shapes[i].bbox();
+  tm.lap("shape boxes");
   sc.order.resize(n);
   for (int i = 0; i < n; ++i) sc.order[i] = i;
-  Builder B{sc.order, boxes, {}, std::vector<float>(n)};
+  Builder B{sc.order, boxes, std::vector<float>(n)};
+  B.spare = build_threads() - 1;
+  std::vector<BNode> ref_nodes;
   if (n > 0) {
-    B.nodes.reserve((size_t)n);
-    B.build(0, n);
+    ref_nodes.reserve((size_t)n);
+    B.build(0, n, ref_nodes);
   }
+  tm.lap("reference median-split tree");
 
   // materials (deduplicated) and primitive records in sorted order
   std::map<std::vector<char>, int> mat_ids;
+  rt_material last_mat{};
+  int last_mid = -1;
   sc.materials.clear();
   sc.prims.assign((size_t)n, rt_prim{});
   bool all_planes = true;
@@ -504,10 +562,12 @@ void build_bvh(Scene& sc) {
     m.transparency = s.mat.transparency;
     m.refractive_index = s.mat.refractive_index;
     m.texture = s.mat.texture;
-    std::vector<char> key((const char*)&m, (const char*)&m + sizeof(m));
-    auto it = mat_ids.find(key);
     int mid;
-    if (it == mat_ids.end()) {
+    if (last_mid >= 0 && std::memcmp(&last_mat, &m, sizeof m) == 0) {
+      mid = last_mid;  // runs of one material (triangle soups): no map lookup
+    } else if (auto it = mat_ids.find(std::vector<char>((const char*)&m, (const char*)&m + sizeof(m)));
+               it == mat_ids.end()) {
+      std::vector<char> key((const char*)&m, (const char*)&m + sizeof(m));
       mid = (int)sc.materials.size();
       mat_ids[key] = mid;
       sc.materials.push_back(m);
@@ -517,6 +577,8 @@ void build_bvh(Scene& sc) {
     } else {
       mid = it->second;
     }
+    last_mat = m;
+    last_mid = mid;
     rt_prim& p = sc.prims[k];
     uint32_t tag = (uint32_t)s.kind | ((uint32_t)mid << 8);
     if (s.kind == RT_PRIM_PLANE) {
@@ -551,11 +613,12 @@ void build_bvh(Scene& sc) {
     }
     std::memcpy(&p.a[15], &tag, 4);
   }
+  tm.lap("materials + primitive records");
   if (sc.materials.empty()) sc.materials.push_back(rt_material{});  // placeholder for empty scenes
   sc.prim_stride = (n > 0 && all_planes) ? 64 : 128;
 
   // scale for pruning / padding margins: scene boxes and the camera
-  for (const BNode& nd : B.nodes)
+  for (const BNode& nd : ref_nodes)
     for (int i = 0; i < 3; ++i) scale = finite_abs_max(finite_abs_max(scale, nd.box.lo[i]), nd.box.hi[i]);
   for (int i = 0; i < 3; ++i) scale = finite_abs_max(scale, sc.camera.location[i]);
   sc.scene_scale = scale;
@@ -563,7 +626,7 @@ void build_bvh(Scene& sc) {
   // the reference's leaves: exact boxes + which leaf holds each sorted position
   std::vector<int> ref_leaf_of(n, 0);
   sc.ref_leaf_boxes.clear();
-  for (const BNode& nd : B.nodes) {
+  for (const BNode& nd : ref_nodes) {
     if (!nd.leaf()) continue;
     int id = (int)(sc.ref_leaf_boxes.size() / 8);
     for (int i = nd.start; i < nd.end; ++i) ref_leaf_of[i] = id;
@@ -571,7 +634,9 @@ void build_bvh(Scene& sc) {
     sc.ref_leaf_boxes.insert(sc.ref_leaf_boxes.end(), v, v + 8);
   }
   sc.tree_depth = 0;
+  tm.lap("reference leaves");
   build_wide(sc, boxes, ref_leaf_of);
+  tm.lap("traversal tree (build_wide)");
   {
     const size_t fl = (size_t)sc.prim_stride / 4;
     const size_t np = sc.prims.size();  // spatial splits may duplicate primitives

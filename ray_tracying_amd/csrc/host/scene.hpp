@@ -2,6 +2,7 @@
 // flattened into the device records of include/rt_hip.h.
 #pragma once
 #include <array>
+#include <chrono>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -75,6 +76,18 @@ struct Scene {
   float scene_scale = 1.0f;
   double load_seconds = 0, build_seconds = 0;
 };
+
+// Phase timings of the host build on stderr when RT_BUILD_TIMING is set (diagnostic).
+struct BuildTimer {
+  const char* what;
+  bool on;
+  double t0, last;
+  explicit BuildTimer(const char* w);
+  void lap(const char* phase);
+};
+
+// Worker threads for the host build: RT_BUILD_THREADS, else the hardware concurrency capped at 16.
+int build_threads();
 
 // Parse and flatten; throws std::runtime_error on unreadable files (the reference's
 // fatal errors), prints the reference's warnings for skipped entries.

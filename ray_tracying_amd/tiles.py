@@ -1,8 +1,9 @@
 """Image-tile data parallelism across GPUs (one process per GPU, torch.distributed).
 
 The reference renders serially (raytracer.cpp:433-476) and has no parallel path; with the
-counter RNG every pixel/sample is independent, so the frame is split into tiles, dealt
-round-robin to ranks (scene content is spatially uneven, so interleaving balances load),
+counter RNG every pixel/sample is independent, so the frame is split into tiles, dealt to
+ranks on a 2-D lattice (tile_rank; scene content is spatially uneven, so interleaving over
+rows and columns balances load),
 rendered independently, and the packed tiles are gathered to rank 0 -- over RCCL/xGMI on
 MI355X (backend "nccl"), over gloo in the CPU tests.  The result is bit-identical for any
 world size (tests/test_distributed.py, tests/test_gpu_parity.py).

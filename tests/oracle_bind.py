@@ -39,6 +39,9 @@ def lib():
         _lib = ctypes.CDLL(ORACLE_SO)
         _lib.oracle_render.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(oracle_params),
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(oracle_stats)]
+        _lib.oracle_render_regions.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(oracle_params),
+                                               ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.POINTER(oracle_stats), ctypes.c_int]
         _lib.oracle_scene_info.argtypes = [ctypes.c_char_p] + [ctypes.POINTER(ctypes.c_int)] * 4
         _lib.oracle_powf.argtypes = [ctypes.c_float, ctypes.c_float]
         _lib.oracle_powf.restype = ctypes.c_float
@@ -75,6 +78,29 @@ def render(path: str, *, use_bvh=True, spp_sqrt=1, light_samples=1, rng=RNG_COUN
         raise RuntimeError(f"oracle_render({path}) -> {rc}")
     return rgb, u8, {"rays": st.rays, "box_tests": st.box_tests, "prim_tests": st.prim_tests,
                      "render_seconds": st.render_seconds, "load_seconds": st.load_seconds}
+
+
+def render_regions(path: str, regions, *, use_bvh=True, spp_sqrt=1, light_samples=1, seed=20251226,
+                   texture_root=None, resolution=None, threads=None):
+    """Counter-RNG render of several (x0, y0, w, h) regions after ONE scene load, rows spread
+    over `threads` threads -> (list of float32 (h, w, 3) arrays, stats dict)."""
+    reg = np.ascontiguousarray(np.asarray(regions, dtype=np.int32).reshape(-1, 4))
+    total = int((reg[:, 2] * reg[:, 3]).sum()) * 3
+    out = np.zeros(total, dtype=np.float32)
+    p = oracle_params(int(use_bvh), int(spp_sqrt), int(light_samples), RNG_COUNTER, int(seed),
+                      resolution[0] if resolution else 0, resolution[1] if resolution else 0, 0, 0, 0, 0)
+    st = oracle_stats()
+    nt = threads or min(16, os.cpu_count() or 1)
+    rc = lib().oracle_render_regions(path.encode(), texture_root.encode() if texture_root else None, ctypes.byref(p),
+                                     len(reg), reg.ctypes.data, out.ctypes.data, ctypes.byref(st), int(nt))
+    if rc:
+        raise RuntimeError(f"oracle_render_regions({path}) -> {rc}")
+    imgs, off = [], 0
+    for x0, y0, w, h in reg.tolist():
+        imgs.append(out[off:off + w * h * 3].reshape(h, w, 3))
+        off += w * h * 3
+    return imgs, {"rays": st.rays, "box_tests": st.box_tests, "prim_tests": st.prim_tests,
+                  "render_seconds": st.render_seconds, "load_seconds": st.load_seconds}
 
 
 def ppm_bytes(u8: np.ndarray) -> bytes:

@@ -123,6 +123,32 @@ def soup(n=200, seed=5, res=(48, 48), light=True) -> dict:
     }
 
 
+def soup_degenerate(n=300, seed=13, res=(48, 48), every=7) -> dict:
+    """A soup in which every `every`-th plane repeats its third corner (c3 == c2): the
+    reference's trap (shapes.cpp:485-494) -- the degenerate sub-triangle
+    (c1, c2, c2) accepts a thin band along the infinite line c1c2 that only the reference's
+    leaf AABB clips, so -bvh and linear disagree and the kernel's unbounded-primitive list is
+    non-empty.  Every `every`-th other plane is a true quad (parallelogram c0, c1, c2, c0+c2-c1)."""
+    sc = soup(n, seed=seed, res=res)
+    for k, pl in enumerate(sc["planes"]):
+        c = pl["corners"]
+        if k % every == 0:
+            c[3] = list(c[2])
+        elif k % every == 3:
+            c[3] = [c[0][i] + c[2][i] - c[1][i] for i in range(3)]
+    return sc
+
+
+def sphere_textured(res=(48, 40)) -> dict:
+    """features() with the checker texture on the spheres (UV from double atan2 / asin,
+    shapes.cpp:257-259; material.hpp:99-134) and on a cube."""
+    sc = features(res=res)
+    for o in sc["spheres"] + sc["cubes"][:1]:
+        if "material" in o:
+            o["material"]["texture_file"] = "checker.jpg"
+    return sc
+
+
 # name -> (scene builder, CLI-equivalent render args).  These are the golden-vector cases.
 def blend(name: str, res=(48, 32), light_radius=None) -> dict:
     with open(os.path.join(GOLDEN, "scenes", "blend", name + ".json")) as f:
@@ -148,6 +174,10 @@ def cases() -> dict:
         "soup_s1": (lambda: soup(300, seed=11), dict(use_bvh=True, spp_sqrt=1, light_samples=1)),
         "soup_s3": (lambda: soup(120, seed=3, res=(32, 32)), dict(use_bvh=True, spp_sqrt=3, light_samples=1)),
         "soup_linear": (lambda: soup(80, seed=4, res=(32, 32)), dict(use_bvh=False, spp_sqrt=1, light_samples=1)),
+        "soup_c3c2_bvh": (lambda: soup_degenerate(400, seed=13), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
+        "soup_c3c2_linear": (lambda: soup_degenerate(150, seed=14, res=(32, 32)),
+                             dict(use_bvh=False, spp_sqrt=1, light_samples=1)),
+        "sphere_textured": (lambda: sphere_textured(), dict(use_bvh=True, spp_sqrt=2, light_samples=2)),
         "blend_c3_antialiasing": (lambda: blend("Antialiasing", (64, 48)), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
         "blend_c4_glossy_soft": (lambda: blend("glossy_reflection", (64, 48), light_radius=1.0),
                                  dict(use_bvh=True, spp_sqrt=2, light_samples=2)),

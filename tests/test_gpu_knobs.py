@@ -35,6 +35,7 @@ KNOBS = [
     {"RT_LEAF_MIN": "64", "RT_REFILL": "1"},
     {"RT_BATCH_SHARDS": "1", "RT_FETCH_SHARDS": "64", "RT_SLOTS": "4096"},
     {"RT_BATCH_SHARDS": "1024", "RT_FETCH_SHARDS": "1"},
+    {"RT_BATCH_SHARDS": "1024", "RT_SLOTS": "4096"},  # more shards than slot-waves: clamped
 ]
 
 
