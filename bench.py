@@ -25,7 +25,7 @@ Scenes of a few primitives (C1-C4) get no roofline claim.
 cpu_baseline: the compiled reference (oracle/_ref/ref_driver; kind "reference") -- or the
 oracle restatement if the reference binary is absent (kind "port") -- on rank 0 at N=1,
 single-threaded, on a bounded row band of the same frame; plus the same band size run as
-concurrent single-threaded processes, one per usable host core (at most 16).
+16 concurrent single-threaded processes (the job's CPU share on the GPU box).
 """
 from __future__ import annotations
 
@@ -87,7 +87,7 @@ def parse():
                     help="SURVEY.md 8(d) C2 BVH-stress variant: the soup without lights (one ray per sample)")
     ap.add_argument("--cpu-procs", type=int, default=min(16, usable_cpus()),
                     help="concurrent reference processes for the multi-core CPU figure (<= 1: skip); default: "
-                         "one per usable host core, at most 16")
+                         "16 (the GPU box's CPU share per job) or fewer if fewer cores are usable")
     ap.add_argument("--pmc-traffic", default=None,
                     help="JSON with per-launch HBM bytes of the trace kernel (tools/pmc_traffic.py); default: the "
                          "committed profile of the headline workload, attached to that workload only")
@@ -158,9 +158,10 @@ def cpu_baseline(scene_path: str, args, rank: int):
             total += stk["rays"]
         out["value_multi_proc"] = sum(rates)
         out["procs"] = n
-        out["host_cpus"] = {"usable": usable_cpus(), "os_cpu_count": os.cpu_count()}
-        out["sample_multi_proc"] = (f"{n} concurrent single-threaded processes (one per usable host core, at most "
-                                    f"16), {band} rows each ({total} rays); value = sum of the per-process rates")
+        out["host_cpus"] = {"affinity": usable_cpus(), "os_cpu_count": os.cpu_count(),
+                            "note": "the GPU pool grants a job 16 host cores whatever the host exposes"}
+        out["sample_multi_proc"] = (f"{n} concurrent single-threaded processes (the job's 16-core CPU share), {band} rows "
+                                    f"each ({total} rays); value = sum of the per-process rates")
     return out
 
 

@@ -195,7 +195,9 @@ int rt_scene_destroy(rt_scene_t scene);
  * tile k occupies [k*tile_w*tile_h*3, (k+1)*tile_w*tile_h*3), row-major RGB, linear
  * (pre-gamma) colour == the reference's compute_pixel_color() result.  Pixels of a tile
  * outside the image are left untouched.  `stream` is a hipStream_t (NULL = default).
- * tile_ids is a HOST array. */
+ * tile_ids is a HOST array.  A call of more than 2^30 samples (RT_MAX_UNITS) runs as
+ * consecutive tile chunks; stats are summed over them.  Replaces the pixel loop of
+ * main() (Code/raytracer.cpp:433-443) calling compute_pixel_color (:18-70). */
 int rt_render_tiles(rt_scene_t scene, const rt_camera_desc* cam, const rt_render_params* params,
                     const int32_t* tile_ids, int32_t n_tiles, int32_t tile_w, int32_t tile_h,
                     float* d_rgb_out, void* stream, rt_stats* stats);

@@ -1432,6 +1432,32 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(RT_EINVAL, "rt_render_tiles: tile id out of range");
   if (stats) *stats = rt_stats{};
   if (n_tiles == 0) return RT_OK;
+  {  // calls larger than the unit cap run as consecutive tile chunks (same pixels: the counter
+     // RNG keys every sample by pixel, so the split changes no value); the per-sample colour
+     // buffer (12 B per unit) stays bounded, and the frame-wide 2^31 unit limit goes away
+    const long long per_tile = (long long)tile_w * tile_h * (p->spp_sqrt <= 1 ? 1LL : (long long)p->spp_sqrt * p->spp_sqrt);
+    long long cap = 1LL << 30;
+    if (const char* e = std::getenv("RT_MAX_UNITS")) cap = std::max(1LL, std::min(cap, std::atoll(e)));
+    if (n_tiles > 1 && (long long)n_tiles * per_tile > cap) {
+      const int k = (int)std::max(1LL, std::min<long long>(n_tiles, cap / per_tile));
+      rt_stats acc{};
+      for (int t0 = 0; t0 < n_tiles; t0 += k) {
+        rt_stats st{};
+        const int rc = rt_render_tiles(s, cam, p, tile_ids + t0, std::min(k, n_tiles - t0), tile_w, tile_h,
+                                       d_out + (size_t)t0 * tile_w * tile_h * 3, stream_ptr, &st);
+        if (rc) return rc;
+        acc.rays += st.rays;
+        acc.box_tests += st.box_tests;
+        acc.prim_tests += st.prim_tests;
+        acc.node_visits += st.node_visits;
+        acc.kernel_ms += st.kernel_ms;
+        acc.trace_ms += st.trace_ms;
+        acc.iterations += st.iterations;
+      }
+      if (stats) *stats = acc;
+      return RT_OK;
+    }
+  }
   const long long n_pixels_ll = (long long)n_tiles * tile_w * tile_h;
   if (n_pixels_ll > 0x7fffffffLL) return fail(RT_EINVAL, "rt_render_tiles: too many pixels in one call");
   const int n_pixels = (int)n_pixels_ll;

@@ -36,6 +36,7 @@ KNOBS = [
     {"RT_BATCH_SHARDS": "1", "RT_FETCH_SHARDS": "64", "RT_SLOTS": "4096"},
     {"RT_BATCH_SHARDS": "1024", "RT_FETCH_SHARDS": "1"},
     {"RT_BATCH_SHARDS": "1024", "RT_SLOTS": "4096"},  # more shards than slot-waves: clamped
+    {"RT_MAX_UNITS": "3000"},  # the call runs as many tile chunks
 ]
 
 
