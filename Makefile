@@ -35,6 +35,13 @@ $(BIN)/raytracer: $(SRC)/host/main.cpp $(LIB)/librt_host.so $(LIB)/librt_comm.so
 	@mkdir -p $(BIN)
 	$(CXX) $(CXXFLAGS) $(SRC)/host/main.cpp -o $@ -L$(LIB) -lrt_host -lrt_comm -lrt_hip -lpthread -Wl,-rpath,'$$ORIGIN/../lib'
 
+# A/B build of the HIP library with extra defines into ray_tracying_amd/lib_$(V)/ (diagnostic;
+# select it at run time with RT_LIB_DIR): make variant V=w5 VDEFS=-DRT_TRACE_WAVES=5
+variant: $(LIB)/librt_host.so
+	@mkdir -p ray_tracying_amd/lib_$(V)
+	$(HIPCC) $(HIPFLAGS) $(VDEFS) -shared $(SRC)/hip/rt_hip.hip -o ray_tracying_amd/lib_$(V)/librt_hip.so
+	cp $(LIB)/librt_host.so ray_tracying_amd/lib_$(V)/
+
 oracle:
 	$(MAKE) -C oracle all
 
@@ -45,4 +52,4 @@ clean:
 	rm -rf $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle ref clean
+.PHONY: all oracle ref clean variant

@@ -510,8 +510,11 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 // `leaf_min` lanes wait on one (or no lane has a node to visit), then they all test their
 // leaf's primitives together -- leaf hits are sparse (~1 per 8 node visits per lane), and
 // testing them at once keeps the primitive code from running with a handful of lanes.
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 4  // waves per SIMD the register allocation targets (A/B builds: make variant)
+#endif
 template <bool kCount, bool kPlanesOnly>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 8))) void trace_refill_kernel(TraceArgs ta) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_slots;
   const int lane = threadIdx.x & 63;
