@@ -16,8 +16,8 @@ roofline: the traversal kernel (trace_refill_kernel) is bo
 VALU issue, not by bytes -- the tree and primitives (~0.1 GB) stay on-die -- so the line
 reports it against the VALU peak: useful lane-operations per second (wave64 VALU
 instructions x 64 x lane utilisation, from the committed rocprofv3 PMC pass of the same
-build) over 256 CUs x 2 wave64 instructions per CU-cycle (SIMD-32: one wave64 VALU
-instruction every 2 cycles per SIMD) x 2.4 GHz.  Beside it, per average trace launch (HIP
+build) over 256 CUs x 1 wave64 instruction per CU-cycle (measured: tools/ubench_valu.hip)
+x 2.4 GHz.  Beside it, per average trace launch (HIP
 events on the launch stream over the timed steps): `hbm` = PMC HBM bytes (traffic) / launch
 time vs 8 TB/s, and `l2` = algorithmic bytes (64 B per BVH4 node visit + 64 B per primitive
 test, counted by an instrumented run of the same frame) / launch time vs the L2's 34.5 TB/s.
@@ -44,10 +44,12 @@ sys.path.insert(0, ROOT)
 METRIC = "Mrays/sec (primary+secondary), 1024x1024 @100spp; % HBM roofline"
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate over 8 XCDs
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-# VALU peak (MI355X_MICROARCH.md "Execution model"): 256 CUs x 4 SIMD-32, a wave64 VALU
-# instruction every 2 cycles per SIMD -> 2 wave64 instructions = 128 lane-ops per CU-cycle
-N_CU, VALU_WAVE_INSTR_PER_CU_CYCLE, MAX_CLOCK_GHZ = 256, 2, 2.4
-VALU_PEAK_TOPS = N_CU * VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3  # 78.6 T lane-ops/s
+# VALU peak: one wave64 VALU instruction per CU-cycle (4 SIMDs, one every 4 cycles each) --
+# measured on the box (tools/ubench_valu.hip, profiles/r02_ubench_valu.txt: independent
+# v_fma_f32 / v_max3_f32 / v_perm_b32 / v_pk_fma_f32 streams saturate at 0.84-0.90 per
+# CU-cycle at 2.4 GHz, 8 waves per SIMD); the guide's 2-cycle SIMD-32 issue is not reached
+N_CU, VALU_WAVE_INSTR_PER_CU_CYCLE, MAX_CLOCK_GHZ = 256, 1, 2.4
+VALU_PEAK_TOPS = N_CU * VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3  # 39.3 T lane-ops/s
 NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
 PMC_PROFILE = "r02_v1"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
@@ -343,8 +345,8 @@ def main():
             "achieved": valu["achieved"] if valu else None, "peak": round(VALU_PEAK_TOPS, 2),
             "unit": "T VALU lane-ops/s", "frac": valu["frac"] if valu else None,
             "traffic": traffic, "traffic_unit": "HBM bytes per trace launch (PMC)", "traffic_source": traffic_src,
-            "peak_definition": "256 CUs x 2 wave64 VALU instructions per CU-cycle (4 SIMD-32) x 64 lanes x 2.4 GHz; "
-                               "achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation",
+            "peak_definition": "256 CUs x 1 wave64 VALU instruction per CU-cycle (measured, profiles/r02_ubench_valu.txt) "
+                               "x 64 lanes x 2.4 GHz; achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation",
             "valu": valu,
             "hbm": {"achieved_gbs": round(hbm_rate, 1) if hbm_rate else None, "peak_gbs": HBM_PEAK_GBS,
                     "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None},

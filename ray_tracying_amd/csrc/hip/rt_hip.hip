@@ -45,12 +45,9 @@ namespace {
 constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
 constexpr int kBlock = 256;
 constexpr int kLdsStack = 16;  // default LDS stack entries per lane (RT_LDS_STACK overrides)
-static int lds_stack_entries() {
-  static const int v = [] {
-    const char* e = std::getenv("RT_LDS_STACK");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : kLdsStack;
-  }();
-  return v;
+static int lds_stack_entries() {  // read per call: tests vary it within one process
+  const char* e = std::getenv("RT_LDS_STACK");
+  return e ? std::max(1, std::min(64, std::atoi(e))) : kLdsStack;
 }
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters

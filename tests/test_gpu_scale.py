@@ -3,8 +3,9 @@ SURVEY.md 8(d) C5 scene; Plane::intersect shapes.cpp:444-494 over the reference'
 median-split leaves acceleration.cpp:20-118).
 
 What only this size exercises: spatial-split duplicate parts (~1.1M primitive records), the
-24-bit leaf packing, depth-12+ trees whose traversal stacks spill past the LDS entries, and a
-frame whose units outnumber the slots, so every slot-wave claims many batches.  The GPU
+24-bit leaf packing, depth-12+ trees (the 64K-slot rerun also cuts the LDS stack to 2
+entries, so deeper entries spill to HBM), and a frame whose units outnumber the slots, so
+every slot-wave claims many batches.  The GPU
 renders a subset of the frame's 64x64 tiles through rt_render_tiles (the path bench.py
 times); the oracle renders the same regions in counter-RNG mode after one scene load
 (oracle_render_regions, rows over host threads).  Bar: every float bit-identical and the
@@ -77,7 +78,7 @@ def test_headline_soup_tiles_1024_100spp(soup_path, gpu):
     off-centre tiles; then the same tiles with only 64K slots (every wave claims ~37
     batches) -- the scheduling must not change a bit."""
     tiles = [7 * 16 + 7, 8 * 16 + 8, 0, 15 * 16 + 15, 8 * 16 + 15, 3 * 16 + 12, 12 * 16 + 4]
-    _check(soup_path, 1024, tiles, 10, seed=SOUP_SEED, slot_variants=({"RT_SLOTS": "65536"},))
+    _check(soup_path, 1024, tiles, 10, seed=SOUP_SEED, slot_variants=({"RT_SLOTS": "65536", "RT_LDS_STACK": "2"},))
 
 
 def test_c5_tile_4096_64spp(soup_path, gpu):

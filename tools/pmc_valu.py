@@ -6,9 +6,9 @@ Usage: pmc_valu.py --dir DIR [--kernel REGEX] --out profiles/x.json
 DIR is the -d directory of `rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU
 SQ_INSTS_VMEM_RD SQ_INSTS_LDS GRBM_GUI_ACTIVE`.  Per dispatch (launches shorter than 50 us --
 the empty last step -- are left out):
-  VALU issue fraction = SQ_INSTS_VALU / (CUs x 2 x cycles): a CU issues at most two wave64
-      VALU instructions per cycle (4 SIMD-32s, 2 cycles each; MI355X_MICROARCH.md "Execution
-      model"); cycles = GRBM_GUI_ACTIVE / XCDs
+  VALU issue fraction = SQ_INSTS_VALU / (CUs x cycles): a CU issues at most one wave64 VALU
+      instruction per cycle (measured: tools/ubench_valu.hip saturates at 0.84-0.90 per
+      CU-cycle for v_fma / v_max3 / v_perm / v_pk_fma); cycles = GRBM_GUI_ACTIVE / XCDs
   lane utilisation   = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU)
 """
 from __future__ import annotations
@@ -20,7 +20,7 @@ import json
 import os
 import re
 
-N_CU, N_XCD, VALU_PER_CU_CYCLE = 256, 8, 2
+N_CU, N_XCD, VALU_PER_CU_CYCLE = 256, 8, 1
 
 
 def main() -> None:
@@ -59,8 +59,8 @@ def main() -> None:
         "lds_per_valu": round(tot["SQ_INSTS_LDS"] / tot["SQ_INSTS_VALU"], 4),
         "per_dispatch_valu_issue_frac": [round(d["SQ_INSTS_VALU"] / (N_CU * VALU_PER_CU_CYCLE * d["GRBM_GUI_ACTIVE"] / N_XCD), 3)
                                          for d in ds],
-        "definition": "VALU issue fraction = wave64 VALU instructions / (256 CUs x 2 x cycles), two per CU-cycle peak "
-                      "(4 SIMD-32, one wave64 instruction per 2 cycles each); "
+        "definition": "VALU issue fraction = wave64 VALU instructions / (256 CUs x cycles), one per CU-cycle peak "
+                      "(measured, tools/ubench_valu.hip); "
                       "lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU)",
     }
     with open(a.out, "w") as fh:
