@@ -507,6 +507,29 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 // `leaf_min` lanes wait on one (or no lane has a node to visit), then they all test their
 // leaf's primitives together -- leaf hits are sparse (~1 per 8 node visits per lane), and
 // testing them at once keeps the primitive code from running with a handful of lanes.
+// RT_PHASE_TIMING (diagnostic A/B builds only): per-wave s_memtime cycles spent in the refill,
+// leaf and node phases of trace_refill_kernel, and how often each runs, summed into the
+// control block (counters 64..71) and printed by rt_render_tiles.
+#ifdef RT_PHASE_TIMING
+#define RT_PT_DECL unsigned long long pt_c[4] = {0, 0, 0, 0}, pt_n[4] = {0, 0, 0, 0}, pt_t = __builtin_amdgcn_s_memtime();
+#define RT_PT_MARK(k)                                           \
+  do {                                                          \
+    const unsigned long long pt_now = __builtin_amdgcn_s_memtime(); \
+    pt_c[k] += pt_now - pt_t;                                   \
+    pt_n[k] += 1;                                               \
+    pt_t = pt_now;                                              \
+  } while (0)
+#define RT_PT_FLUSH                                               \
+  if (lane == 0)                                                  \
+    for (int k = 0; k < 4; ++k) {                                 \
+      atomicAdd(ta.counters + 64 + k, pt_c[k]);                   \
+      atomicAdd(ta.counters + 68 + k, pt_n[k]);                   \
+    }
+#else
+#define RT_PT_DECL
+#define RT_PT_MARK(k)
+#define RT_PT_FLUSH
+#endif
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 4  // waves per SIMD the register allocation targets (A/B builds: make variant)
 #endif
@@ -536,7 +559,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
   int sp = 0;
   const LaneStack S{reinterpret_cast<int2*>(lds_stack) + threadIdx.x, reinterpret_cast<int2*>(a.spill)};
+  RT_PT_DECL
   for (;;) {
+    RT_PT_MARK(3);  // loop control (ballots) since the node phase
     uint64_t act = __ballot(item != kNoItem);
     if (__popcll(act) < a.refill_min) {
       if (slot >= 0 && item == kNoItem) {
@@ -593,6 +618,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
         q_next += min(avail, (unsigned)__popcll(freem));
       }
       act = __ballot(item != kNoItem);
+      RT_PT_MARK(0);  // refill: write-back, work fetch, query setup
       if (act == 0ull && exhausted) break;
     }
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
@@ -605,10 +631,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
         lim = cull_limit(a, q, h);
         item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
       }
+      RT_PT_MARK(1);  // leaf phase
     }
     // node phase
+#ifdef RT_PHASE_TIMING
+    if (__ballot(item >= 0) != 0ull) {
+      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+      RT_PT_MARK(2);  // node phase
+    }
+#else
     if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+#endif
   }
+  RT_PT_FLUSH
   trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
 }
 
@@ -1687,6 +1722,15 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     stats->kernel_ms = ms;
     stats->trace_ms = trace_ms;
     stats->iterations = iters;
+#ifdef RT_PHASE_TIMING
+    {
+      unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      HIP_TRY(hipMemcpy(pt, ctl + 4 + 2 * 64, sizeof(pt), hipMemcpyDeviceToHost), RT_EDEVICE);
+      const double tot = (double)(pt[0] + pt[1] + pt[2] + pt[3]);
+      std::fprintf(stderr, "[rt phase] refill %.3f (%llu), leaf %.3f (%llu), node %.3f (%llu), control %.3f (%llu) of %.3g wave-ticks\n",
+                   pt[0] / tot, pt[4], pt[1] / tot, pt[5], pt[2] / tot, pt[6], pt[3] / tot, pt[7], tot);
+    }
+#endif
     stats->node_visits = 0;
     if (p->count_work) {  // lane-level node visits (trace_counters_out, ctl byte 488)
       unsigned long long nv = 0;
