@@ -45,6 +45,9 @@ extern "C" {
 #define RT_TAG_KIND(tag) ((tag) & 3u)
 #define RT_TAG_PLANE_VALID 4u       /* Plane: |cross(c1-c0,c2-c0)| >= 1e-6f (shapes.cpp:450) */
 #define RT_TAG_MOVING 8u            /* Sphere with non-zero velocity (shapes.cpp:207-209) */
+#define RT_TAG_TRI1_NEVER 16u       /* Plane with c3 == c0 whose first sub-triangle (c1,c3,c2) cannot
+                                       accept a hit point within sqrt(a[12]) of c0 (then a[12] holds
+                                       that radius squared instead of c3.x; c3 = c0): scene.cpp */
 #define RT_TAG_MATERIAL(tag) ((tag) >> 8)
 
 /* One primitive, 128 bytes (64-byte stride when every primitive is a Plane).

@@ -216,15 +216,22 @@ template <bool kAttr>
 __device__ __forceinline__ bool plane_hit(const PrimA& P, const Ray& ray, float& t_out, HitAttr* at,
                                           V3* x_out = nullptr) {
   if (!(prim_tag(P) & RT_TAG_PLANE_VALID)) return false;
+  const bool tri = (prim_tag(P) & RT_TAG_TRI1_NEVER) != 0u;
   V3 c0{P.a[0], P.a[1], P.a[2]}, c1{P.a[4], P.a[5], P.a[6]}, c2{P.a[8], P.a[9], P.a[10]};
-  V3 c3{P.a[12], P.a[13], P.a[14]};
+  V3 c3 = tri ? c0 : V3{P.a[12], P.a[13], P.a[14]};
   V3 n{P.a[3], P.a[7], P.a[11]};
   float denom = dot(n, ray.d);
   if (fabsf(denom) < 1e-6f) return false;
   float t = ((dot(sub(c0, ray.o), n)) / (denom));
   if (t < 0) return false;
   V3 X{ray.o.x + t * ray.d.x, ray.o.y + t * ray.d.y, ray.o.z + t * ray.d.z};
-  if (!in_tri(X, c1, c3, c2, n) && !in_tri(X, c0, c1, c2, n)) return false;
+  // isPointInQuad: (c1, c3, c2) || (c0, c1, c2); the OR of two pure tests in either order.  With
+  // RT_TAG_TRI1_NEVER the first cannot accept a point within sqrt(a[12]) of c0 (scene.cpp).
+  if (!in_tri(X, c0, c1, c2, n)) {
+    const V3 dx = sub(X, c0);
+    if (tri && dot(dx, dx) <= P.a[12]) return false;
+    if (!in_tri(X, c1, c3, c2, n)) return false;
+  }
   t_out = t;
   if (x_out) *x_out = X;
   if (kAttr) {

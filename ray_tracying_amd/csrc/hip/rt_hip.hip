@@ -195,7 +195,8 @@ __device__ __forceinline__ bool plane_leaf_fast_ok(const PrimA& P, const Ray& r,
   bool ok = true;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const float c0 = P.a[k], c1 = P.a[4 + k], c2 = P.a[8 + k], c3 = P.a[12 + k];
+    const float c0 = P.a[k], c1 = P.a[4 + k], c2 = P.a[8 + k];
+    const float c3 = (prim_tag(P) & RT_TAG_TRI1_NEVER) ? c0 : P.a[12 + k];  // a[12] is a radius then
     const float lo = fminf(fminf(c0, c1), fminf(c2, c3)) - 1e-4f;
     const float hi = fmaxf(fmaxf(c0, c1), fmaxf(c2, c3)) + 1e-4f;
     const float p = o[k] + t * d[k];

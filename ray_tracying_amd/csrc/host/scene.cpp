@@ -515,6 +515,37 @@ struct Builder {
   }
 };
 
+// isPointInQuad's first sub-triangle (c1, c3, c2) (shapes.cpp:485-494) with c3 == c0 has the
+// opposite winding to the normal: its three edge functions e_i = dot(cross(B-A, P-A), n) sum to
+// S = dot(A x B + B x C + C x A, n) < 0 for every point P.  isPointInTriangle (shapes.cpp:24-40)
+// accepts only if all three float e_i >= -1e-6, i.e. (with float error |e_i - exact| <=
+// 32 * 2^-24 * |E_i| * |P - A_i|) only if S >= -3e-6 - sum of the errors.  For |P - c0| <= R
+// (|P - A_i| <= R + Emax) that is impossible when |S| - 3e-6 > 96 * 2^-24 * Emax * (R + Emax).
+// Returns half of the largest such R (0 if none): the kernel skips the test for hit points
+// within R of c0 -- same result, fewer instructions.
+double tri1_never_radius(const V3& A, const V3& B, const V3& C, const V3& n) {
+  auto d3 = [](const V3& v) { return std::array<double, 3>{v[0], v[1], v[2]}; };
+  auto cross = [](const std::array<double, 3>& a, const std::array<double, 3>& b) {
+    return std::array<double, 3>{a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  };
+  const auto a = d3(A), b = d3(B), c = d3(C), nn = d3(n);
+  const auto ab = cross(a, b), bc = cross(b, c), ca = cross(c, a);
+  double S = 0, mag = 0;
+  for (int k = 0; k < 3; ++k) {
+    S += (ab[k] + bc[k] + ca[k]) * nn[k];
+    mag += (std::fabs(ab[k]) + std::fabs(bc[k]) + std::fabs(ca[k])) * std::fabs(nn[k]);
+  }
+  if (!(S < 0)) return 0.0;
+  auto len = [](const std::array<double, 3>& u, const std::array<double, 3>& v) {
+    return std::sqrt((u[0] - v[0]) * (u[0] - v[0]) + (u[1] - v[1]) * (u[1] - v[1]) + (u[2] - v[2]) * (u[2] - v[2]));
+  };
+  const double emax = std::max({len(a, b), len(b, c), len(c, a)});
+  const double slack = -S - 3e-6 - 1e-12 * mag;  // double rounding of S: far below 1e-12 * mag
+  if (!(slack > 0) || !(emax > 0)) return 0.0;
+  const double r = slack / (96.0 * std::ldexp(1.0, -24) * emax) - emax;
+  return r > 0 ? 0.5 * r : 0.0;
+}
+
 float finite_abs_max(float a, float b) {
   if (!std::isfinite(b)) return a;
   return std::max(a, std::fabs(b));
@@ -599,6 +630,13 @@ void build_bvh(Scene& sc) {
       p.a[12] = c[3][0];
       p.a[13] = c[3][1];
       p.a[14] = c[3][2];
+      if ((tag & RT_TAG_PLANE_VALID) && c[3] == c[0]) {
+        const double r = tri1_never_radius(c[1], c[0], c[2], un);
+        if (r > 0.0) {  // a[12] = R^2 (rounded down); c3 == c0 is implied by the tag
+          tag |= RT_TAG_TRI1_NEVER;
+          p.a[12] = std::nextafter((float)(r * r), 0.0f);
+        }
+      }
     } else {
       all_planes = false;
       for (int r = 0; r < 3; ++r)

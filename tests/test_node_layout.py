@@ -50,6 +50,8 @@ def check_tree(sc):
     covered = np.zeros(d.n_prims, np.int64)
     is_plane = (prims[:, 15].view(np.uint32) & 3) == 3
     corners = prims[:, [0, 1, 2, 4, 5, 6, 8, 9, 10, 12, 13, 14]].reshape(-1, 4, 3).astype(np.float64)
+    tri1 = (prims[:, 15].view(np.uint32) & 16) != 0  # RT_TAG_TRI1_NEVER: c3 == c0, a[12] holds a radius
+    corners[tri1, 3] = corners[tri1, 0]
     checked = 0
     # spatial splits: a primitive may sit in several leaves (parts); every corner of a plane
     # must lie inside all ancestor boxes of at least one of its parts
