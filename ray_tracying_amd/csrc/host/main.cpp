@@ -62,7 +62,11 @@ int main(int argc, char* argv[]) {
 
   rth_scene_t scene = nullptr;
   if (rth_scene_load(scene_file.c_str(), textures.c_str(), res_w, res_h, &scene) != 0) {
-    std::cerr << "An error occurred: " << rth_last_error() << std::endl;
+    // a zero resolution is main()'s own check (raytracer.cpp:399-402), printed bare; loader
+    // exceptions reach main()'s catch (raytracer.cpp:482-485)
+    const std::string e = rth_last_error();
+    if (e.rfind("Error: Camera resolution is 0", 0) == 0) std::cerr << e << std::endl;
+    else std::cerr << "An error occurred: " << e << std::endl;
     return 1;
   }
   rth_scene_info info{};

@@ -400,20 +400,38 @@ struct Loader {
 std::unique_ptr<Scene> load_scene(const std::string& path, const std::string& texture_root, int res_w, int res_h) {
   auto t0 = std::chrono::steady_clock::now();
   auto sc = std::make_unique<Scene>();
-  std::string text = slurp(path);
+  // main() reads the camera first (raytracer.cpp:396-404): Camera(path) reports an unreadable
+  // or malformed file and falls back to resolution 0, which ends the run before the lights
+  // and shapes are loaded (camera.cpp:14-58, 240-252); -res (no reference counterpart) skips
+  // that stop, and the loaders' own errors then apply (json_loader.cpp:106-116)
+  const bool res_override = res_w > 0 && res_h > 0;
+  const char* kResZero = "Error: Camera resolution is 0. Check scene.json.";
+  auto camera_failed = [&](const std::string& loader_error) {
+    std::cerr << "Camera configuration failed to load. Using default values." << std::endl;
+    throw std::runtime_error(res_override ? loader_error : std::string(kResZero));
+  };
+  std::string text;
+  try {
+    text = slurp(path);
+  } catch (std::runtime_error& e) {
+    std::cerr << "Error: Could not open file " << path << std::endl;
+    camera_failed(e.what());
+  }
   std::unique_ptr<JsonDoc> doc;
   try {
     doc = std::make_unique<JsonDoc>(text);
   } catch (JsonError& e) {
-    throw std::runtime_error(std::string("Error: JSON parsing error: ") + e.what());
+    std::cerr << "JSON Parse Error: " << e.what() << std::endl;
+    camera_failed(std::string("Error: JSON parsing error: ") + e.what());
   }
   { std::string().swap(text); }
   Loader L{*doc, *sc, texture_root, path, {}};
   L.camera();
-  if (res_w > 0 && res_h > 0) {
+  if (res_override) {
     sc->camera.res_x = res_w;
     sc->camera.res_y = res_h;
   }
+  if (sc->camera.res_x == 0 || sc->camera.res_y == 0) throw std::runtime_error(kResZero);
   L.lights();
   L.shapes();
   doc.reset();

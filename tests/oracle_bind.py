@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+ORACLE_SO = os.environ.get("ORACLE_SO") or os.path.join(ROOT, "oracle", "liboracle.so")  # ORACLE_SO: sanitizer build
 RNG_MT19937, RNG_COUNTER = 0, 1
 
 
