@@ -60,6 +60,10 @@ constexpr int kCtrStride = 32;
 // reads their any_query copies.  Steps after the frame's last query find every slot-wave
 // retired (logic) and no query (trace) and return at once, so a batch may overshoot.
 constexpr int kMaxHostBatch = 16;
+// Slot pipelines: the slots are split into independent logic -> trace pipelines on their own
+// streams, so one pipeline's logic step and launch tail overlap the other's traversal.
+constexpr int kPipes = 2;
+constexpr size_t kFetchLines = (size_t)kMaxFetchShards + 1;  // fetch counters + any_query, per pipeline
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
@@ -120,7 +124,8 @@ struct LogicArgs {
   float* samples;  // [n_units][3] per-sample Trace colours
   float* out;
   // buffers
-  int n_slots;
+  int n_slots;           // field stride of every per-slot array (all pipelines' slots)
+  int slot_base, slot_end;  // this pipeline's slots [slot_base, slot_end) (multiples of kBlock)
   uint32_t* state;
   uint32_t* frames;      // [kMaxDepth][FR_COUNT][n_slots] (null if no reflection/refraction)
   float* refr;           // [kMaxDepth][6][n_slots] (null if no refraction)
@@ -145,7 +150,8 @@ struct TraceArgs {
   int fetch_shards;
   const unsigned int* any_query;  // logic's "some slot has a query" flag for this step
   unsigned long long* rays;   // queries traced (one atomic per wave at exit)
-  int n_slots;
+  int n_slots;                // field stride of the per-slot arrays
+  int slot_base, n_work;      // this pipeline's query slots: [slot_base, slot_base + n_work)
   int lds_entries;            // traversal stack entries kept in LDS per lane
   int* spill;                 // deeper entries: [entry - lds_entries][n_threads]
   int n_threads;              // threads of the persistent grid
@@ -537,7 +543,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 template <bool kCount, bool kPlanesOnly>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
-  const unsigned int nq = (unsigned)ta.n_slots;
+  const unsigned int nq = (unsigned)ta.n_work;
   const int lane = threadIdx.x & 63;
   const uint64_t lane_lt = (1ull << lane) - 1ull;
   unsigned int nrays = 0;
@@ -583,8 +589,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
               base = __shfl(base, 0);
             }
             if (len > 0 && base < len) {
-              q_next = st0 + base;
-              q_end = st0 + min(base + 64u, len);
+              q_next = (unsigned)ta.slot_base + st0 + base;
+              q_end = (unsigned)ta.slot_base + st0 + min(base + 64u, len);
               // 64-slot groups are slot-waves of the logic step: skip one whose slots retired
               if (a.wave_done[q_next >> 6] != 0u) continue;
               break;
@@ -732,11 +738,11 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
 #endif
 template <bool kFrames, bool kTex, bool kPlanes>
 __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
-  const int slot = blockIdx.x * kBlock + threadIdx.x;
+  const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
   // a wave whose slots all retired has nothing left in this frame (one scalar load)
   if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
   bool want = false;
-  if (slot < a.n_slots) {
+  if (slot < a.slot_end) {
     const int N = a.n_slots;
     uint32_t* S = a.state;
     auto ld = [&](int f) { return S[f * N + slot]; };
@@ -1305,11 +1311,13 @@ struct rt_scene_s {
   float* d_hit = nullptr;
   unsigned int* d_wave_done = nullptr;
   size_t slots_cap = 0;
-  unsigned int* h_flag = nullptr;  // pinned: one 128-B line per step of a host batch (any_query copies)
+  unsigned int* h_flag = nullptr;  // pinned: per pipeline, one 128-B line per step of a host batch (any_query copies)
   unsigned int* d_batch_ctr = nullptr;  // kMaxBatchShards counters, one 128-B line each
-  unsigned int* d_fetch = nullptr;      // trace fetch counters (one line each) + any_query line
-  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;
-  hipEvent_t ev_a[kMaxHostBatch] = {}, ev_b[kMaxHostBatch] = {};  // per step of a host batch: around the trace launch
+  unsigned int* d_fetch = nullptr;      // per pipeline: trace fetch counters (one line each) + any_query line
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_fork = nullptr, ev_join = nullptr;
+  // per pipeline and step of a host batch: around the trace launch
+  hipEvent_t ev_a[kPipes][kMaxHostBatch] = {}, ev_b[kPipes][kMaxHostBatch] = {};
+  hipStream_t aux[kPipes] = {};  // pipelines 1.. run on these non-blocking streams (0: the caller's)
   int last_iters = 0;  // steps the previous render took: the size of the next render's first host batch
 };
 
@@ -1363,12 +1371,15 @@ int rt_scene_destroy(rt_scene_t s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
-  hipEvent_t evs[] = {s->ev_t0, s->ev_t1};
+  hipEvent_t evs[] = {s->ev_t0, s->ev_t1, s->ev_fork, s->ev_join};
   for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
-  for (int k = 0; k < kMaxHostBatch; ++k) {
-    if (s->ev_a[k]) (void)hipEventDestroy(s->ev_a[k]);
-    if (s->ev_b[k]) (void)hipEventDestroy(s->ev_b[k]);
+  for (int h = 0; h < kPipes; ++h) {
+    for (int k = 0; k < kMaxHostBatch; ++k) {
+      if (s->ev_a[h][k]) (void)hipEventDestroy(s->ev_a[h][k]);
+      if (s->ev_b[h][k]) (void)hipEventDestroy(s->ev_b[h][k]);
+    }
+    if (s->aux[h]) (void)hipStreamDestroy(s->aux[h]);
   }
   delete s;
   return RT_OK;
@@ -1424,13 +1435,18 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     return rc;
   }
   bool ev_ok = true;
-  for (int k = 0; k < kMaxHostBatch && ev_ok; ++k)
-    ev_ok = hipEventCreate(&s->ev_a[k]) == hipSuccess && hipEventCreate(&s->ev_b[k]) == hipSuccess;
+  for (int h = 0; h < kPipes && ev_ok; ++h) {
+    for (int k = 0; k < kMaxHostBatch && ev_ok; ++k)
+      ev_ok = hipEventCreate(&s->ev_a[h][k]) == hipSuccess && hipEventCreate(&s->ev_b[h][k]) == hipSuccess;
+    ev_ok = ev_ok && (h == 0 || hipStreamCreateWithFlags(&s->aux[h], hipStreamNonBlocking) == hipSuccess);
+  }
   if (!ev_ok || hipMalloc(&s->d_ctl, kCtlBytes) != hipSuccess ||
-      hipHostMalloc((void**)&s->h_flag, (size_t)kMaxHostBatch * kFetchStride * 4) != hipSuccess ||
+      hipHostMalloc((void**)&s->h_flag, (size_t)kPipes * kMaxHostBatch * kFetchStride * 4) != hipSuccess ||
       hipMalloc(&s->d_batch_ctr, (size_t)kMaxBatchShards * kCtrStride * 4) != hipSuccess ||
-      hipMalloc(&s->d_fetch, ((size_t)kMaxFetchShards + 1) * kFetchStride * 4) != hipSuccess ||
-      hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess) {
+      hipMalloc(&s->d_fetch, (size_t)kPipes * kFetchLines * kFetchStride * 4) != hipSuccess ||
+      hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
     rt_scene_destroy(s);
     return fail(RT_ENOMEM, "rt_scene_create: control block / events");
   }
@@ -1589,7 +1605,6 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.hit = s->d_hit;
   la.late_draws = s->late_draws ? 1 : 0;
   la.pinhole = cam->aperture <= 0.0f ? 1 : 0;
-  la.any_query = s->d_fetch + (size_t)fetch_shards_env() * kFetchStride;  // the line after the fetch counters
   la.wave_done = s->d_wave_done;
   la.batch_ctr = s->d_batch_ctr;
   // every shard needs a slot-wave to drain it (wave w claims from shard w % batch_shards)
@@ -1606,9 +1621,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.result = s->d_result;
   ta.hit = s->d_hit;
   ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
-  ta.fetch = s->d_fetch;
   ta.fetch_shards = fetch_shards_env();
-  ta.any_query = la.any_query;
   ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
@@ -1617,97 +1630,162 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.refill_min = refill_min_env();
   ta.leaf_min = leaf_min_env();
   ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
-  const unsigned trace_blocks = (unsigned)std::max(1, std::min(s->n_cu * s->trace_blocks_per_cu,
-                                                               (n_slots + kBlock - 1) / kBlock));
-  ta.n_threads = (int)trace_blocks * kBlock;
-  const int spill_entries = std::max(0, s->desc.stack_bound - ta.lds_entries);
-  if ((size_t)spill_entries * ta.n_threads > s->spill_cap) {
-    if (s->d_spill) (void)hipFree(s->d_spill);
-    s->d_spill = nullptr;
-    s->spill_cap = 0;
-    HIP_TRY(hipMalloc(&s->d_spill, (size_t)spill_entries * ta.n_threads * sizeof(int2)), RT_ENOMEM);
-    s->spill_cap = (size_t)spill_entries * ta.n_threads;
-  }
-  ta.spill = s->d_spill;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
   // entry + t_near per stack slot
   const size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
+
+  int replay_iter = -1, replay_reps = 0;
+  const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
+  if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
+  // the diagnostics wait on every step (one pipeline)
+  const bool step_sync = diag || replay_iter >= 0;
+
+  // ---- pipelines: the slots split into kPipes independent logic -> trace sequences, one per
+  // stream (units are claimed from the shared batch counters, so the split changes no value).
+  // A pipeline's logic step and the tail of its trace launch run while the other pipeline's
+  // traversal fills the machine.  Small calls (or RT_PIPES=1) keep one pipeline.
+  int n_pipes = n_slots >= (1 << 20) ? kPipes : 1;
+  if (const char* e = std::getenv("RT_PIPES")) n_pipes = std::max(1, std::min(kPipes, std::atoi(e)));
+  if (step_sync || n_slots < kPipes * kBlock) n_pipes = 1;
+  struct Pipe {
+    LogicArgs la;
+    TraceArgs ta;
+    hipStream_t st;
+    unsigned logic_blocks, trace_blocks;
+    int iters;
+    bool done;
+  } pipes[kPipes];
+  const int per_pipe = (n_slots / kBlock / n_pipes) * kBlock;
+  const int spill_entries = std::max(0, s->desc.stack_bound - ta.lds_entries);
+  const unsigned grid_cap = (unsigned)std::max(1, s->n_cu * s->trace_blocks_per_cu);
+  size_t spill_need = 0;
+  for (int h = 0; h < n_pipes; ++h) {
+    Pipe& P = pipes[h];
+    const int base = h * per_pipe, count = h == n_pipes - 1 ? n_slots - base : per_pipe;
+    P.st = h == 0 ? stream : s->aux[h];
+    P.la = la;
+    P.la.slot_base = base;
+    P.la.slot_end = base + count;
+    P.ta = ta;
+    P.ta.slot_base = base;
+    P.ta.n_work = count;
+    P.ta.fetch = s->d_fetch + (size_t)h * kFetchLines * kFetchStride;
+    P.la.any_query = P.ta.fetch + (size_t)ta.fetch_shards * kFetchStride;  // the line after the fetch counters
+    P.ta.any_query = P.la.any_query;
+    P.logic_blocks = (unsigned)(count / kBlock);
+    P.trace_blocks = std::min(grid_cap, (unsigned)((count + kBlock - 1) / kBlock));
+    P.ta.n_threads = (int)P.trace_blocks * kBlock;
+    spill_need += (size_t)spill_entries * P.ta.n_threads;
+    P.iters = 0;
+    P.done = false;
+  }
+  if (spill_need > s->spill_cap) {
+    if (s->d_spill) (void)hipFree(s->d_spill);
+    s->d_spill = nullptr;
+    s->spill_cap = 0;
+    HIP_TRY(hipMalloc(&s->d_spill, spill_need * sizeof(int2)), RT_ENOMEM);
+    s->spill_cap = spill_need;
+  }
+  for (int h = 0, off = 0; h < n_pipes; ++h) {  // each pipeline's traversal spills into its own range
+    pipes[h].ta.spill = s->d_spill + (size_t)2 * off;
+    off += spill_entries * pipes[h].ta.n_threads;
+  }
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result,
                      s->d_query, s->d_wave_done);
   HIP_TRY(hipGetLastError(), RT_EDEVICE);
 
-  // ---- iterate logic -> trace until no slot issues a query
+  // ---- iterate logic -> trace per pipeline until none of its slots issues a query
   double trace_ms = 0.0;
   int iters = 0;
-  int replay_iter = -1, replay_reps = 0;
-  const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
   unsigned long long diag_prev = 0;
-  if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
   // steps go out in host batches (one wait per batch, not per step); the first batch is
-  // sized by the previous render's step count, the diagnostics wait on every step
-  const bool step_sync = diag || replay_iter >= 0;
+  // sized by the previous render's step count
   int batch = step_sync ? 1 : std::max(2, std::min(kMaxHostBatch, s->last_iters + 1));
   HIP_TRY(hipEventRecord(s->ev_t0, stream), RT_EDEVICE);
-  for (bool done = false; !done;) {
-   for (int k = 0; k < batch; ++k) {
-    // per-step reset: trace work counters + any_query (the line after them)
-    HIP_TRY(hipMemsetAsync(s->d_fetch, 0, ((size_t)ta.fetch_shards + 1) * kFetchStride * 4, stream), RT_EDEVICE);
-    launch_logic(la, need_frames, (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0, planes_only, slot_blocks, stream);
-    HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipMemcpyAsync(s->h_flag + (size_t)k * kFetchStride, la.any_query, 4, hipMemcpyDeviceToHost, stream),
-            RT_EDEVICE);
-    HIP_TRY(hipEventRecord(s->ev_a[k], stream), RT_EDEVICE);
-    launch_trace(ta, p->count_work != 0, planes_only, trace_blocks, lds, stream);
-    HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipEventRecord(s->ev_b[k], stream), RT_EDEVICE);
-   }
-   HIP_TRY(hipEventSynchronize(s->ev_b[batch - 1]), RT_EDEVICE);
-   for (int k = 0; k < batch && !done; ++k) {
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[k], s->ev_b[k]), RT_EDEVICE);
-    if (replay_iter == iters && replay_reps > 0 && !p->count_work) {  // batch == 1 here
-      // diagnostic (RT_TRACE_REPLAY=iter:reps): re-trace this step's queries; the results
-      // are recomputed identically, so the frame is unchanged
-      float tot = 0.f, best = 1e30f;
-      unsigned long long rays0 = 0;
-      HIP_TRY(hipMemcpy(&rays0, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-      for (int r = 0; r < replay_reps; ++r) {
-        HIP_TRY(hipMemsetAsync(s->d_fetch, 0, (size_t)ta.fetch_shards * kFetchStride * 4, stream), RT_EDEVICE);
-        HIP_TRY(hipEventRecord(s->ev_a[1], stream), RT_EDEVICE);
-        launch_trace(ta, false, planes_only, trace_blocks, lds, stream);
-        HIP_TRY(hipEventRecord(s->ev_b[1], stream), RT_EDEVICE);
-        HIP_TRY(hipEventSynchronize(s->ev_b[1]), RT_EDEVICE);
-        float m = 0.f;
-        HIP_TRY(hipEventElapsedTime(&m, s->ev_a[1], s->ev_b[1]), RT_EDEVICE);
-        tot += m;
-        best = std::min(best, m);
-      }
-      unsigned long long rays1 = 0;
-      HIP_TRY(hipMemcpy(&rays1, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-      HIP_TRY(hipMemcpy(ctl + 8, &rays0, 8, hipMemcpyHostToDevice), RT_EDEVICE);  // keep the frame's ray count
-      std::fprintf(stderr, "[rt replay] step %d: %llu queries, trace %.4f ms avg / %.4f ms min over %d reps\n", iters,
-                   (rays1 - rays0) / (unsigned long long)replay_reps, tot / replay_reps, best, replay_reps);
-    }
-    const bool more = s->h_flag[(size_t)k * kFetchStride] != 0;
-    if (diag && more) {
-      unsigned long long rc = 0;
-      HIP_TRY(hipMemcpy(&rc, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-      std::fprintf(stderr, "[rt diag] step %2d: %9llu queries, trace %.3f ms (%.2f Gq/s)\n", iters, rc - diag_prev, ms,
-                   (double)(rc - diag_prev) / (ms * 1e6));
-      diag_prev = rc;
-    }
-    if (more) {  // the final (empty) trace launch -- and any after it in the batch -- is not a traversal step
-      trace_ms += ms;
-      ++iters;
-    } else {
-      done = true;
-    }
-   }
-   batch = step_sync ? 1 : 4;  // the previous render's count fell short: top up in small batches
+  if (n_pipes > 1) {  // the other pipelines start after init (and the resets before it)
+    HIP_TRY(hipEventRecord(s->ev_fork, stream), RT_EDEVICE);
+    for (int h = 1; h < n_pipes; ++h) HIP_TRY(hipStreamWaitEvent(pipes[h].st, s->ev_fork, 0), RT_EDEVICE);
   }
-  s->last_iters = iters;
+  const bool tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
+  for (int live = n_pipes; live > 0;) {
+    for (int h = 0; h < n_pipes; ++h) {
+      Pipe& P = pipes[h];
+      if (P.done) continue;
+      unsigned int* flag = s->h_flag + (size_t)h * kMaxHostBatch * kFetchStride;
+      for (int k = 0; k < batch; ++k) {
+        // per-step reset: trace work counters + any_query (the line after them)
+        HIP_TRY(hipMemsetAsync(P.ta.fetch, 0, ((size_t)ta.fetch_shards + 1) * kFetchStride * 4, P.st), RT_EDEVICE);
+        launch_logic(P.la, need_frames, tex, planes_only, P.logic_blocks, P.st);
+        HIP_TRY(hipGetLastError(), RT_EDEVICE);
+        HIP_TRY(hipMemcpyAsync(flag + (size_t)k * kFetchStride, P.la.any_query, 4, hipMemcpyDeviceToHost, P.st),
+                RT_EDEVICE);
+        HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
+        launch_trace(P.ta, p->count_work != 0, planes_only, P.trace_blocks, lds, P.st);
+        HIP_TRY(hipGetLastError(), RT_EDEVICE);
+        HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
+      }
+    }
+    for (int h = 0; h < n_pipes; ++h) {
+      Pipe& P = pipes[h];
+      if (P.done) continue;
+      const unsigned int* flag = s->h_flag + (size_t)h * kMaxHostBatch * kFetchStride;
+      HIP_TRY(hipEventSynchronize(s->ev_b[h][batch - 1]), RT_EDEVICE);
+      for (int k = 0; k < batch && !P.done; ++k) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[h][k], s->ev_b[h][k]), RT_EDEVICE);
+        if (replay_iter == iters && replay_reps > 0 && !p->count_work) {  // one pipeline, batch == 1 here
+          // diagnostic (RT_TRACE_REPLAY=iter:reps): re-trace this step's queries; the results
+          // are recomputed identically, so the frame is unchanged
+          float tot = 0.f, best = 1e30f;
+          unsigned long long rays0 = 0;
+          HIP_TRY(hipMemcpy(&rays0, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+          for (int r = 0; r < replay_reps; ++r) {
+            HIP_TRY(hipMemsetAsync(P.ta.fetch, 0, (size_t)ta.fetch_shards * kFetchStride * 4, stream), RT_EDEVICE);
+            HIP_TRY(hipEventRecord(s->ev_a[0][1], stream), RT_EDEVICE);
+            launch_trace(P.ta, false, planes_only, P.trace_blocks, lds, stream);
+            HIP_TRY(hipEventRecord(s->ev_b[0][1], stream), RT_EDEVICE);
+            HIP_TRY(hipEventSynchronize(s->ev_b[0][1]), RT_EDEVICE);
+            float m = 0.f;
+            HIP_TRY(hipEventElapsedTime(&m, s->ev_a[0][1], s->ev_b[0][1]), RT_EDEVICE);
+            tot += m;
+            best = std::min(best, m);
+          }
+          unsigned long long rays1 = 0;
+          HIP_TRY(hipMemcpy(&rays1, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+          HIP_TRY(hipMemcpy(ctl + 8, &rays0, 8, hipMemcpyHostToDevice), RT_EDEVICE);  // keep the frame's ray count
+          std::fprintf(stderr, "[rt replay] step %d: %llu queries, trace %.4f ms avg / %.4f ms min over %d reps\n", iters,
+                       (rays1 - rays0) / (unsigned long long)replay_reps, tot / replay_reps, best, replay_reps);
+        }
+        const bool more = flag[(size_t)k * kFetchStride] != 0;
+        if (diag && more) {
+          unsigned long long rc = 0;
+          HIP_TRY(hipMemcpy(&rc, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+          std::fprintf(stderr, "[rt diag] step %2d: %9llu queries, trace %.3f ms (%.2f Gq/s)\n", iters, rc - diag_prev, ms,
+                       (double)(rc - diag_prev) / (ms * 1e6));
+          diag_prev = rc;
+        }
+        if (more) {  // the final (empty) trace launch -- and any after it in the batch -- is not a traversal step
+          trace_ms += ms;
+          ++iters;
+          ++P.iters;
+        } else {
+          P.done = true;
+          --live;
+        }
+      }
+    }
+    batch = step_sync ? 1 : 4;  // the previous render's count fell short: top up in small batches
+  }
+  if (n_pipes > 1) {  // reduce after every pipeline's last step
+    for (int h = 1; h < n_pipes; ++h) {
+      HIP_TRY(hipEventRecord(s->ev_join, pipes[h].st), RT_EDEVICE);
+      HIP_TRY(hipStreamWaitEvent(stream, s->ev_join, 0), RT_EDEVICE);
+    }
+  }
+  s->last_iters = 0;
+  for (int h = 0; h < n_pipes; ++h) s->last_iters = std::max(s->last_iters, pipes[h].iters);
   hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
   HIP_TRY(hipGetLastError(), RT_EDEVICE);
   HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
