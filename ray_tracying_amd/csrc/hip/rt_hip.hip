@@ -82,8 +82,28 @@ enum Field : int {
                       // nothing for a pinhole camera, whose primary rays start at its location)
   F_COUNT = F_RAY + 7
 };
-// closest-hit record written by the trace kernel, one per slot: point, normal, u, v, material
-enum HitField : int { HIT_P = 0, HIT_N = 3, HIT_U = 6, HIT_V = 7, HIT_MAT = 8, HIT_COUNT = 9 };
+// closest-hit record written by the trace kernel, one per slot, AoS (48 B: stored from one
+// address by the trace kernel -- no per-field base pointers held in the traversal loop --
+// and read as three float4 by the logic step): point, normal, u, v, material
+enum HitField : int { HIT_P = 0, HIT_N = 3, HIT_U = 6, HIT_V = 7, HIT_MAT = 8, HIT_STRIDE = 12 };
+struct HitRec {
+  V3 p, n;
+  float u, v;
+  uint32_t mat;
+};
+__device__ __forceinline__ float* hit_rec(float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
+__device__ __forceinline__ const float* hit_rec(const float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
+// point + normal + material (u, v untouched)
+__device__ __forceinline__ void store_hit_pnm(float* R, V3 p, V3 n, uint32_t mat) {
+  *reinterpret_cast<float4*>(R) = make_float4(p.x, p.y, p.z, n.x);
+  *reinterpret_cast<float2*>(R + 4) = make_float2(n.y, n.z);
+  R[HIT_MAT] = __uint_as_float(mat);
+}
+__device__ __forceinline__ HitRec load_hit(const float* R) {
+  const float4 a = *reinterpret_cast<const float4*>(R), b = *reinterpret_cast<const float4*>(R + 4),
+               c = *reinterpret_cast<const float4*>(R + 8);
+  return HitRec{V3{a.x, a.y, a.z}, V3{a.w, b.x, b.y}, b.z, b.w, __float_as_uint(c.x)};
+}
 // query record, one per slot: o(3) d(3); TMAX = light distance (shadow) or ray time
 // (closest); KIND bit 0 = shadow any-hit
 enum QField : int { Q_O = 0, Q_D = 3, Q_TMAX = 6, Q_KIND = 7, Q_COUNT = 8 };
@@ -131,7 +151,7 @@ struct LogicArgs {
   float* refr;           // [kMaxDepth][6][n_slots] (null if no refraction)
   float* query;          // [Q_COUNT][n_slots]
   const int* result;     // [n_slots]
-  const float* hit;      // [HIT_COUNT][n_slots] (closest hits)
+  const float* hit;      // [n_slots][HIT_STRIDE] (closest hits)
   int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
@@ -156,7 +176,7 @@ struct TraceArgs {
   int* spill;                 // deeper entries: [entry - lds_entries][n_threads]
   int n_threads;              // threads of the persistent grid
   unsigned long long* counters;  // box tests, prim tests (count_work)
-  float* hit;                 // [HIT_COUNT][n_slots]: attributes of a closest hit (for the logic step)
+  float* hit;                 // [n_slots][HIT_STRIDE]: attributes of a closest hit (for the logic step)
   int has_tex;                // some material is textured: hit u, v needed
   int refill_min;             // refill kernel: refill finished lanes when fewer than this many traverse
   int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
@@ -172,10 +192,6 @@ struct HitState {
   int best_ref;   // reference index of the best hit (tie-break, acceleration.cpp:112)
   int best_idx;   // primitive index (traversal order) of the best hit, -1 = miss
   bool done;      // any-hit: occluded
-  // planes-only scenes: the best hit's record, kept when it is found (Plane::intersect's hit
-  // point and the precomputed normal, shapes.cpp:472-480) so the write-back needs no re-test
-  V3 p, n;
-  uint32_t mat;
 };
 
 // The reference accepts a primitive's hit only if its reference leaf box passes the exact
@@ -211,9 +227,14 @@ __device__ __forceinline__ bool plane_leaf_fast_ok(const PrimA& P, const Ray& r,
   return ok;
 }
 
+// Tests primitives [first, first + cnt) against the lane's query.  Planes-only scenes without
+// textures store a new closest hit's record (Plane::intersect's hit point and the precomputed
+// normal, shapes.cpp:472-480, and the material) to the slot's hit record when it is found --
+// a closer hit overwrites it -- so the write-back needs no re-test and no register holds it
+// across the traversal.
 template <bool kCount, bool kPlanesOnly>
-__device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cnt, const Ray& r, bool any, float tmax,
-                                           uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
+__device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int first, int cnt, const Ray& r, bool any,
+                                           float tmax, uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
   for (int k = 0; k < cnt; ++k) {
     const int pi = first + k;
     const float4* rec = a.c.prims + (size_t)pi * a.c.prim_stride4;
@@ -246,10 +267,8 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
       h.best_t = t;
       h.best_ref = ref.x;
       h.best_idx = pi;
-      if (kPlanesOnly) {
-        h.p = X;
-        h.n = V3{P.a[3], P.a[7], P.a[11]};
-        h.mat = RT_TAG_MATERIAL(prim_tag(P));
+      if (kPlanesOnly && !a.has_tex) {
+        store_hit_pnm(hit_rec(a.hit, slot), X, V3{P.a[3], P.a[7], P.a[11]}, RT_TAG_MATERIAL(prim_tag(P)));
       }
     }
   }
@@ -276,15 +295,11 @@ struct Query {
                     // picks the lo word (inv_i >= 0), 0x07060504 the hi word
 };
 
-// Reads slot's query record; false if the slot emitted no query this step.
-__device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query& q) {
-  const int N = a.n_slots;
-  const int kind = __float_as_int(a.query[Q_KIND * N + slot]);
-  if (kind < 0) return false;
-  q.r.o = V3{a.query[(Q_O + 0) * N + slot], a.query[(Q_O + 1) * N + slot], a.query[(Q_O + 2) * N + slot]};
-  q.r.d = V3{a.query[(Q_D + 0) * N + slot], a.query[(Q_D + 1) * N + slot], a.query[(Q_D + 2) * N + slot]};
-  const float tq = a.query[Q_TMAX * N + slot];
-  q.any = (kind & 1) != 0;
+// The traversal form of a query: origin, direction, light distance (shadow) or ray time.
+__device__ __forceinline__ void setup_query(Query& q, V3 o, V3 d, float tq, bool any) {
+  q.r.o = o;
+  q.r.d = d;
+  q.any = any;
   q.tmax = q.any ? tq : 0.0f;
   q.r.time = q.any ? 0.0f : tq;  // shadow rays have time 0 (raytracer.cpp:225, shapes.hpp:28)
   uint32_t par = 0;
@@ -302,27 +317,38 @@ __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query&
   q.sel[0] = q.inv.x < 0.0f ? 0x07060504u : 0x03020100u;
   q.sel[1] = q.inv.y < 0.0f ? 0x07060504u : 0x03020100u;
   q.sel[2] = q.inv.z < 0.0f ? 0x07060504u : 0x03020100u;
+}
+
+// Reads slot's query record; false if the slot emitted no query this step.
+__device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query& q) {
+  const int N = a.n_slots;
+  const int kind = __float_as_int(a.query[Q_KIND * N + slot]);
+  if (kind < 0) return false;
+  setup_query(q, V3{a.query[(Q_O + 0) * N + slot], a.query[(Q_O + 1) * N + slot], a.query[(Q_O + 2) * N + slot]},
+              V3{a.query[(Q_D + 0) * N + slot], a.query[(Q_D + 1) * N + slot], a.query[(Q_D + 2) * N + slot]},
+              a.query[Q_TMAX * N + slot], (kind & 1) != 0);
   return true;
 }
 
-// After the traversal: the primitives whose region could not be boxed, then the result
-// word and (closest hits) the hit record the logic step shades.
+// After the traversal: the primitives whose region could not be boxed (tested by every ray).
+template <bool kCount, bool kPlanesOnly>
+__device__ __forceinline__ void complete_query(const TraceArgs& a, int slot, const Query& q, HitState& h,
+                                               unsigned int& nprim) {
+  if (a.c.use_bvh && !h.done && a.n_unbounded > 0)
+    test_prims<kCount, kPlanesOnly>(a, slot, a.c.n_prims - a.n_unbounded, a.n_unbounded, q.r, q.any, q.tmax, q.par, true, h,
+                                    nprim);
+}
+
+// The result word and (closest hits) the hit record the logic step shades (planes-only scenes
+// without textures: already stored by test_prims when the hit was found).
 template <bool kCount, bool kPlanesOnly>
 __device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const Query& q, HitState& h,
                                              unsigned int& nprim) {
   const int N = a.n_slots;
   const Ray& r = q.r;
-  // primitives whose accepted region is not boxable: tested by every ray
-  if (a.c.use_bvh && !h.done && a.n_unbounded > 0)
-    test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, r, q.any, q.tmax, q.par, true, h, nprim);
+  complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
   a.result[slot] = q.any ? (h.done ? 1 : 0) : h.best_idx;
-  if (kPlanesOnly && !a.has_tex && !q.any && h.best_idx >= 0) {
-    // the record captured when the hit was found (no uv without textures)
-    float* H = a.hit;
-    H[(HIT_P + 0) * N + slot] = h.p.x; H[(HIT_P + 1) * N + slot] = h.p.y; H[(HIT_P + 2) * N + slot] = h.p.z;
-    H[(HIT_N + 0) * N + slot] = h.n.x; H[(HIT_N + 1) * N + slot] = h.n.y; H[(HIT_N + 2) * N + slot] = h.n.z;
-    H[HIT_MAT * N + slot] = __uint_as_float(h.mat);
-  } else if (!q.any && h.best_idx >= 0) {
+  if (!(kPlanesOnly && !a.has_tex) && !q.any && h.best_idx >= 0) {
     // the hit record the Trace/shade step needs (raytracer.cpp:293-303): the same
     // primitive test with attributes, on the primitive this lane just tested (cached)
     const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
@@ -333,13 +359,9 @@ __device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const
     if (a.has_tex) prim_hit<true, kPlanesOnly, true>(P, rec, r, t, &at);
     else prim_hit<true, kPlanesOnly, false>(P, rec, r, t, &at);
     float* H = a.hit;
-    H[(HIT_P + 0) * N + slot] = at.p.x; H[(HIT_P + 1) * N + slot] = at.p.y; H[(HIT_P + 2) * N + slot] = at.p.z;
-    H[(HIT_N + 0) * N + slot] = at.n.x; H[(HIT_N + 1) * N + slot] = at.n.y; H[(HIT_N + 2) * N + slot] = at.n.z;
-    if (a.has_tex) {
-      H[HIT_U * N + slot] = at.u;
-      H[HIT_V * N + slot] = at.v;
-    }
-    H[HIT_MAT * N + slot] = __uint_as_float(RT_TAG_MATERIAL(prim_tag(P)));
+    float* R = hit_rec(a.hit, slot);
+    store_hit_pnm(R, at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
+    if (a.has_tex) *reinterpret_cast<float2*>(R + HIT_U) = make_float2(at.u, at.v);
   }
 }
 
@@ -566,15 +588,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
   int sp = 0;
   const LaneStack S{reinterpret_cast<int2*>(lds_stack) + threadIdx.x, reinterpret_cast<int2*>(a.spill)};
+  // a query was set up in q: start its traversal at the root (BVH::intersect_linear tests
+  // every primitive at once, acceleration.cpp:124-139, and leaves nothing to traverse)
+  auto start_traversal = [&]() {
+    h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
+    lim = cull_limit(a, q, h);
+    sp = 0;
+    item = (a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem;
+    if (a.c.n_prims > 0 && !a.c.use_bvh)
+      test_prims<kCount, kPlanesOnly>(a, slot, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
+  };
+  // the lane's query is complete: write it back and free the lane
+  auto settle = [&]() {
+    finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+    slot = -1;
+  };
   RT_PT_DECL
   for (;;) {
     RT_PT_MARK(3);  // loop control (ballots) since the node phase
     uint64_t act = __ballot(item != kNoItem);
     if (__popcll(act) < a.refill_min) {
-      if (slot >= 0 && item == kNoItem) {
-        finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
-        slot = -1;
-      }
+      if (slot >= 0 && item == kNoItem) settle();
       while (!exhausted) {
         const uint64_t freem = __ballot(slot < 0);
         if (freem == 0ull) break;
@@ -610,30 +644,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
             slot = s;
             ++nrays;
             if (kCount && q.any) ++dg_any_rays;
-            h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
-            lim = cull_limit(a, q, h);
-            sp = 0;
-            item = (a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem;
-            if (a.c.n_prims > 0 && !a.c.use_bvh)  // BVH::intersect_linear (acceleration.cpp:124-139)
-              test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
-            if (item == kNoItem) {  // nothing to traverse: write back at once
-              finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
-              slot = -1;
-            }
+            start_traversal();  // nothing to traverse (linear mode): settled in the next refill phase
           }
         }
         q_next += min(avail, (unsigned)__popcll(freem));
       }
       act = __ballot(item != kNoItem);
       RT_PT_MARK(0);  // refill: write-back, work fetch, query setup
-      if (act == 0ull && exhausted) break;
+      // done when the queue is drained and every lane settled (a query with nothing to
+      // traverse -- linear mode, empty scene -- is settled in the next refill phase)
+      if (exhausted && __ballot(slot >= 0) == 0ull) break;
     }
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
     const uint64_t leafm = __ballot(is_leaf_item(item));
     if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
       if (is_leaf_item(item)) {
         const uint32_t e = (uint32_t)item;
-        test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
+        test_prims<kCount, kPlanesOnly>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
                                         true, h, nprim);
         lim = cull_limit(a, q, h);
         item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
@@ -781,14 +808,14 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       const V3 cam_o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
       if (st0 == ST_SHADOW || st0 == ST_CLOSEST) {
         // the hit being shaded: the trace kernel's record (prim_hit<true> on the hit primitive)
-        const float* H = a.hit;
-        hp = V3{H[(HIT_P + 0) * N + slot], H[(HIT_P + 1) * N + slot], H[(HIT_P + 2) * N + slot]};
-        hn = V3{H[(HIT_N + 0) * N + slot], H[(HIT_N + 1) * N + slot], H[(HIT_N + 2) * N + slot]};
+        const HitRec hr = load_hit(hit_rec(a.hit, slot));
+        hp = hr.p;
+        hn = hr.n;
         if (kTex) {
-          hu = H[HIT_U * N + slot];
-          hv = H[HIT_V * N + slot];
+          hu = hr.u;
+          hv = hr.v;
         }
-        mat_id = (int)__float_as_uint(H[HIT_MAT * N + slot]);
+        mat_id = (int)hr.mat;
       }
       if (st0 == ST_SHADOW) {
         const uint32_t lw = ld(F_LIGHT);
@@ -1546,7 +1573,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_state, N * F_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_hit, N * HIT_COUNT * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_hit, N * HIT_STRIDE * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_wave_done, (N / 64 + 1) * 4), RT_ENOMEM);
     if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
     if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
