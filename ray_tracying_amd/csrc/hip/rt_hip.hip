@@ -106,7 +106,26 @@ __device__ __forceinline__ HitRec load_hit(const float* R) {
 }
 // query record, one per slot: o(3) d(3); TMAX = light distance (shadow) or ray time
 // (closest); KIND bit 0 = shadow any-hit
+// SoA [field][slot] (an AoS record of two float4 measured no faster for the trace kernel and
+// cost the logic kernel registers: 132 VGPRs at the same occupancy target)
 enum QField : int { Q_O = 0, Q_D = 3, Q_TMAX = 6, Q_KIND = 7, Q_COUNT = 8 };
+struct QueryRec {
+  V3 o, d;
+  float tq;
+  int kind;
+};
+__device__ __forceinline__ QueryRec load_query(const float* Q, int N, int slot) {
+  return QueryRec{V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]},
+                  V3{Q[(Q_D + 0) * N + slot], Q[(Q_D + 1) * N + slot], Q[(Q_D + 2) * N + slot]},
+                  Q[Q_TMAX * N + slot], __float_as_int(Q[Q_KIND * N + slot])};
+}
+__device__ __forceinline__ void store_query(float* Q, int N, int slot, V3 o, V3 d, float tq, int kind) {
+  Q[(Q_O + 0) * N + slot] = o.x; Q[(Q_O + 1) * N + slot] = o.y; Q[(Q_O + 2) * N + slot] = o.z;
+  Q[(Q_D + 0) * N + slot] = d.x; Q[(Q_D + 1) * N + slot] = d.y; Q[(Q_D + 2) * N + slot] = d.z;
+  Q[Q_TMAX * N + slot] = tq;
+  Q[Q_KIND * N + slot] = __int_as_float(kind);
+}
+__device__ __forceinline__ void store_no_query(float* Q, int N, int slot) { Q[Q_KIND * N + slot] = __int_as_float(-1); }
 // frames for depths 0..kMaxDepth-1: A(3) + meta, and the pending refraction ray (6)
 enum FrField : int { FR_A = 0, FR_META = 3, FR_COUNT = 4 };
 
@@ -151,7 +170,7 @@ struct LogicArgs {
   float* refr;           // [kMaxDepth][6][n_slots] (null if no refraction)
   float* query;          // [Q_COUNT][n_slots]
   const int* result;     // [n_slots]
-  const float* hit;      // [n_slots][HIT_STRIDE] (closest hits)
+  float* hit;            // [n_slots][HIT_STRIDE] (closest hits; written here for transformed shapes)
   int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
@@ -348,20 +367,21 @@ __device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const
   const Ray& r = q.r;
   complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
   a.result[slot] = q.any ? (h.done ? 1 : 0) : h.best_idx;
-  if (!(kPlanesOnly && !a.has_tex) && !q.any && h.best_idx >= 0) {
-    // the hit record the Trace/shade step needs (raytracer.cpp:293-303): the same
-    // primitive test with attributes, on the primitive this lane just tested (cached)
+  if (kPlanesOnly && a.has_tex && !q.any && h.best_idx >= 0) {
+    // textured planes: the hit record with (u, v) -- the same primitive test with attributes,
+    // on the primitive this lane just tested (cached).  Scenes with transformed shapes get
+    // their record from the logic step (logic_kernel, ST_CLOSEST): sphere / cube / rectangle
+    // attributes (double atan2 / asin UVs, object-to-world transforms) would push this
+    // kernel past its 128 registers.
     const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
     PrimA P;
     load_prim_a(rec, P);
     HitAttr at;
     float t;
-    if (a.has_tex) prim_hit<true, kPlanesOnly, true>(P, rec, r, t, &at);
-    else prim_hit<true, kPlanesOnly, false>(P, rec, r, t, &at);
-    float* H = a.hit;
+    prim_hit<true, true, true>(P, rec, r, t, &at);
     float* R = hit_rec(a.hit, slot);
     store_hit_pnm(R, at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
-    if (a.has_tex) *reinterpret_cast<float2*>(R + HIT_U) = make_float2(at.u, at.v);
+    *reinterpret_cast<float2*>(R + HIT_U) = make_float2(at.u, at.v);
   }
 }
 
@@ -760,11 +780,19 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
 // kFrames: some material reflects or refracts (Trace recursion frames needed)
 // kTex: some material has a texture (hit UVs + texel fetch)
 // kPlanes: every primitive is a Plane (no transformed-shape intersection code)
+// Waves per SIMD the register allocation must allow (__launch_bounds__' second argument:
+// blocks of 4 waves per CU = waves per SIMD).  The logic step is bound by the latency of its
+// scattered state loads, so occupancy pays: without frames 4 waves (<= 128 VGPRs; the
+// unconstrained allocation took 132 = 3 waves, 10 % slower frame); with recursion frames
+// the state machine needs ~195 (2 waves).  A/B builds: make variant VDEFS=-DRT_LOGIC_WAVES=5
 #ifndef RT_LOGIC_WAVES
-#define RT_LOGIC_WAVES 1
+#define RT_LOGIC_WAVES 4
+#endif
+#ifndef RT_LOGIC_WAVES_F
+#define RT_LOGIC_WAVES_F 2
 #endif
 template <bool kFrames, bool kTex, bool kPlanes>
-__global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
+__global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
   const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
   // a wave whose slots all retired has nothing left in this frame (one scalar load)
   if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
@@ -806,8 +834,29 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       V3 hp{0.0f, 0.0f, 0.0f}, hn{0.0f, 0.0f, 0.0f}, fin{0.0f, 0.0f, 0.0f};
       float vis = 0.0f, hu = 0.0f, hv = 0.0f;
       const V3 cam_o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
-      if (st0 == ST_SHADOW || st0 == ST_CLOSEST) {
-        // the hit being shaded: the trace kernel's record (prim_hit<true> on the hit primitive)
+      if (!kPlanes && st0 == ST_CLOSEST && res_ld >= 0) {
+        // the hit being shaded (raytracer.cpp:293-303): the hit primitive's test with
+        // attributes on the ray just traced (the query record), kept in the slot's hit record
+        // for the shadow steps that follow
+        const QueryRec qr = load_query(a.query, N, slot);
+        const Ray tr{qr.o, qr.d, qr.tq};
+        const float4* rec = a.c.prims + (size_t)res_ld * a.c.prim_stride4;
+        PrimA P;
+        load_prim_a(rec, P);
+        HitAttr at;
+        float t;
+        prim_hit<true, false, kTex>(P, rec, tr, t, &at);
+        hp = at.p;
+        hn = at.n;
+        hu = at.u;
+        hv = at.v;
+        mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
+        float* R = hit_rec(a.hit, slot);
+        store_hit_pnm(R, hp, hn, (uint32_t)mat_id);
+        if (kTex) *reinterpret_cast<float2*>(R + HIT_U) = make_float2(hu, hv);
+      } else if (st0 == ST_SHADOW || st0 == ST_CLOSEST) {
+        // the hit being shaded: its record (written by the trace kernel for planes-only scenes,
+        // by the ST_CLOSEST step above otherwise)
         const HitRec hr = load_hit(hit_rec(a.hit, slot));
         hp = hr.p;
         hn = hr.n;
@@ -831,13 +880,15 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
         if (ls > 0) vis = ldf(F_VIS);
         if (light > 0) fin = V3{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
       } else if (st0 == ST_CLOSEST) {
-        const float* Q = a.query;
         if (kFrames) {
-          ray.o = V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]};
-          ray.d = V3{Q[(Q_D + 0) * N + slot], Q[(Q_D + 1) * N + slot], Q[(Q_D + 2) * N + slot]};
-          ray.time = Q[Q_TMAX * N + slot];  // closest queries carry the ray time there
+          const QueryRec qr = load_query(a.query, N, slot);
+          ray.o = qr.o;
+          ray.d = qr.d;
+          ray.time = qr.tq;  // closest queries carry the ray time there
+        } else if (!a.pinhole) {
+          ray.o = load_query(a.query, N, slot).o;
         } else {
-          ray.o = a.pinhole ? cam_o : V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]};
+          ray.o = cam_o;
         }
       }
       const int res = st0 >= ST_CLOSEST ? res_ld : -1;
@@ -1107,10 +1158,10 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
       if (__ballot(!retired) == 0ull && (threadIdx.x & 63) == 0) a.wave_done[slot >> 6] = 1u;
       if (retired) {
         stu(F_UNIT, 0xFFFFFFFFu);
-        a.query[Q_KIND * N + slot] = __int_as_float(-1);
+        store_no_query(a.query, N, slot);
       } else if (!want) {  // idle: keep the state, no query this step
         stu(F_UNIT, (uint32_t)-2);
-        a.query[Q_KIND * N + slot] = __int_as_float(-1);
+        store_no_query(a.query, N, slot);
       } else {
         if (fresh) stu(F_UNIT, (uint32_t)unit);  // a query without a new sample keeps its unit
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
@@ -1135,11 +1186,7 @@ __global__ __launch_bounds__(kBlock, RT_LOGIC_WAVES) void logic_kernel(LogicArgs
             }
           }
         }
-        float* Q = a.query;
-        Q[(Q_O + 0) * N + slot] = qo.x; Q[(Q_O + 1) * N + slot] = qo.y; Q[(Q_O + 2) * N + slot] = qo.z;
-        Q[(Q_D + 0) * N + slot] = qd.x; Q[(Q_D + 1) * N + slot] = qd.y; Q[(Q_D + 2) * N + slot] = qd.z;
-        Q[Q_TMAX * N + slot] = qtmax;
-        Q[Q_KIND * N + slot] = __int_as_float(qkind);
+        store_query(a.query, N, slot, qo, qd, qtmax, qkind);
       }
     }
   }
@@ -1229,7 +1276,7 @@ __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slo
   if ((slot & 63) == 0) wave_done[slot >> 6] = 0u;
   state[F_CTRL * n_slots + slot] = ST_SAMPLE;
   result[slot] = -1;
-  query[Q_KIND * n_slots + slot] = __int_as_float(-1);
+  store_no_query(query, n_slots, slot);
 }
 
 template <bool F, bool T>
@@ -1667,11 +1714,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // the diagnostics wait on every step (one pipeline)
   const bool step_sync = diag || replay_iter >= 0;
 
-  // ---- pipelines: the slots split into kPipes independent logic -> trace sequences, one per
-  // stream (units are claimed from the shared batch counters, so the split changes no value).
-  // A pipeline's logic step and the tail of its trace launch run while the other pipeline's
-  // traversal fills the machine.  Small calls (or RT_PIPES=1) keep one pipeline.
-  int n_pipes = n_slots >= (1 << 20) ? kPipes : 1;
+  // ---- pipelines: the slots may split into kPipes independent logic -> trace sequences, one
+  // per stream (units are claimed from the shared batch counters, so the split changes no
+  // value): a pipeline's logic step and the tail of its trace launch then run while the other
+  // pipeline's traversal fills the machine.  Measured (same box, A/B): headline +0.8 %, one
+  // rank's share of an 8-way split -1 %, C4 (92 short steps) -5 %; so one pipeline unless
+  // RT_PIPES=2 asks for two.
+  int n_pipes = 1;
   if (const char* e = std::getenv("RT_PIPES")) n_pipes = std::max(1, std::min(kPipes, std::atoi(e)));
   if (step_sync || n_slots < kPipes * kBlock) n_pipes = 1;
   struct Pipe {

@@ -3,7 +3,8 @@
 Each knob is read once per process (environment), so every configuration renders in a fresh
 child process and must match the oracle bit for bit: the LDS traversal stack cut to 2
 entries (every deeper entry spills to HBM), extreme refill / leaf-phase thresholds, one and
-many work-counter shards, and a slot count so small that a frame takes dozens of steps.
+many work-counter shards, a slot count so small that a frame takes dozens of steps, and the
+slots split into two pipelines on two streams.
 """
 import os
 import subprocess
@@ -37,6 +38,8 @@ KNOBS = [
     {"RT_BATCH_SHARDS": "1024", "RT_FETCH_SHARDS": "1"},
     {"RT_BATCH_SHARDS": "1024", "RT_SLOTS": "4096"},  # more shards than slot-waves: clamped
     {"RT_MAX_UNITS": "3000"},  # the call runs as many tile chunks
+    {"RT_PIPES": "2"},  # two slot pipelines on two streams
+    {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
 ]
 
 
