@@ -130,6 +130,9 @@ __device__ __forceinline__ void store_no_query(float* Q, int N, int slot) { Q[Q_
 enum FrField : int { FR_A = 0, FR_META = 3, FR_COUNT = 4 };
 
 enum : int { ST_SAMPLE = 0, ST_CLOSEST = 1, ST_SHADOW = 2 };
+// result word of a shadow query that shadow_step_kernel consumed in this step (results are
+// otherwise >= -1: a primitive index, -1 for a miss, or 0 / 1 for a shadow query)
+constexpr int kResAdvanced = -2;
 
 struct Common {
   const float4* prims;
@@ -169,10 +172,11 @@ struct LogicArgs {
   uint32_t* frames;      // [kMaxDepth][FR_COUNT][n_slots] (null if no reflection/refraction)
   float* refr;           // [kMaxDepth][6][n_slots] (null if no refraction)
   float* query;          // [Q_COUNT][n_slots]
-  const int* result;     // [n_slots]
+  int* result;           // [n_slots] (shadow_step_kernel marks consumed results)
   float* hit;            // [n_slots][HIT_STRIDE] (closest hits; written here for transformed shapes)
   int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
+  int multi_shadow;      // some light has radius > 0 and light_samples > 1: shadow_step_kernel runs first
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
   unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it)
 };
@@ -826,6 +830,10 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
       // is known: a miss ignores it); a shadow result needs the hit and the shade
       // accumulators; a new sample needs nothing.
       const int st0 = unit >= 0 ? st : -1;
+      // A shadow result whose light still had soft-shadow samples to draw was advanced by
+      // shadow_step_kernel earlier in this step (it marks the consumed result -2): such a
+      // slot is left untouched here and only counts as a slot with a query.
+      const bool fast = st0 == ST_SHADOW && res_ld == kResAdvanced;
       int light = 0, ls = 0, mat_id = 0;
       Ray ray;
       ray.o = V3{0.0f, 0.0f, 0.0f};
@@ -834,7 +842,9 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
       V3 hp{0.0f, 0.0f, 0.0f}, hn{0.0f, 0.0f, 0.0f}, fin{0.0f, 0.0f, 0.0f};
       float vis = 0.0f, hu = 0.0f, hv = 0.0f;
       const V3 cam_o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
-      if (!kPlanes && st0 == ST_CLOSEST && res_ld >= 0) {
+      if (fast) {
+        want = true;
+      } else if (!kPlanes && st0 == ST_CLOSEST && res_ld >= 0) {
         // the hit being shaded (raytracer.cpp:293-303): the hit primitive's test with
         // attributes on the ray just traced (the query record), kept in the slot's hit record
         // for the shadow steps that follow
@@ -866,7 +876,7 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
         }
         mat_id = (int)hr.mat;
       }
-      if (st0 == ST_SHADOW) {
+      if (st0 == ST_SHADOW && !fast) {
         const uint32_t lw = ld(F_LIGHT);
         light = (int)(lw & 0xffffu);
         ls = (int)(lw >> 16);
@@ -892,76 +902,23 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
         }
       }
       const int res = st0 >= ST_CLOSEST ? res_ld : -1;
-      int px = 0, py = 0, sample = 0;
-      // the pixel / sample coordinates (64-bit division, tile lookups) are only needed when a
-      // sample starts; later steps continue its RNG stream from the stored key and counter
+      // later steps of a sample continue its RNG stream from the stored key and counter
       Rng rng;
       rng.key = 0;
       rng.ctr = 0;
-      bool fresh = false;  // a sample started in this step: its RNG key goes to the state
       if (st0 >= ST_CLOSEST) {
         rng.key = (uint64_t)key_lo | ((uint64_t)key_hi << 32);
         rng.ctr = rng_ctr;
       }
-      bool retired = false;
-      bool idle = unit == -2;
+      bool idle = st0 < 0;  // idle (batch done, pixel outside the image): start_kernel's work
       V3 qo{0, 0, 0}, qd{0, 0, 0};
       float qtmax = 0.0f;
       int qkind = 0;
 
-     for (int pass = 0; pass < 2; ++pass) {
-      if (pass == 1) {
-        // the whole wave finished its batch: pull the next 64 consecutive samples (one pixel's
-        // worth -> coherent rays) from this wave's counter shard
-        const int wave = (int)(slot >> 6);
-        const int shard = wave % a.batch_shards;
-        const int leader = __ffsll((long long)__ballot(1)) - 1;  // lowest active lane
-        unsigned int j = 0;
-        if ((threadIdx.x & 63) == leader) j = atomicAdd(a.batch_ctr + shard * kCtrStride, 1u);
-        j = __shfl(j, leader);
-        const long long batch = (long long)j * a.batch_shards + shard;
-        unit = batch * 64 + (threadIdx.x & 63);
-        idle = false;
-        if (batch * 64 >= a.n_units || unit >= a.n_units) {
-          retired = true;
-        } else {
-          const bool inside = unit_coords(a, unit, px, py, sample);
-          st = ST_SAMPLE;
-          if (!inside) idle = true;  // edge tile: pixel outside the image
-        }
-      }
-      while (!want && !retired && !idle) {
+      while (!want && !idle) {
         V3 ret{0, 0, 0};
         bool returning = false;
         bool shade_now = false;
-        if (st == ST_SAMPLE) {
-          // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)
-          rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
-          fresh = true;
-          float fx, fy;
-          if (s <= 1) {
-            fx = (float)px + 0.5f;
-            fy = (float)py + 0.5f;
-          } else {
-            int si = sample % s, sj = sample / s;
-            double ox = rng.next();
-            double oy = rng.next();
-            double sx = ((double)si + ox) / (double)s;
-            double sy = ((double)sj + oy) / (double)s;
-            fx = (float)((double)px + sx);
-            fy = (float)((double)py + sy);
-          }
-          ray = camera_ray(a.cam, fx, fy, rng);
-          ray.time = (float)rng.next();
-          depth = 0;
-          st = ST_CLOSEST;
-          qo = ray.o;
-          qd = ray.d;
-          qtmax = ray.time;
-          qkind = 0;
-          want = true;
-          break;
-        }
         if (st == ST_CLOSEST) {  // Trace body after get_intersection (raytracer.cpp:293-303)
           if (res < 0) {
             ret = V3{0.1f, 0.1f, 0.1f};
@@ -1152,26 +1109,14 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
           }
         }
       }
-      // pass 2 only when no lane of the wave has a query and the wave is not finished
-      if (__ballot(want || (!idle && !retired)) != 0ull || __ballot(!retired) == 0ull) break;
-     }
-      if (__ballot(!retired) == 0ull && (threadIdx.x & 63) == 0) a.wave_done[slot >> 6] = 1u;
-      if (retired) {
-        stu(F_UNIT, 0xFFFFFFFFu);
-        store_no_query(a.query, N, slot);
-      } else if (!want) {  // idle: keep the state, no query this step
+      if (fast || st0 < 0) {
+        // advanced by shadow_step_kernel / idle since an earlier step: nothing changes
+      } else if (!want) {  // the sample finished: idle until the wave's batch is done
         stu(F_UNIT, (uint32_t)-2);
         store_no_query(a.query, N, slot);
       } else {
-        if (fresh) stu(F_UNIT, (uint32_t)unit);  // a query without a new sample keeps its unit
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
-        if (a.late_draws) {
-          stu(F_RNG, rng.ctr);
-          if (fresh) {
-            stu(F_KEY, (uint32_t)rng.key);
-            stu(F_KEY + 1, (uint32_t)(rng.key >> 32));
-          }
-        }
+        if (a.late_draws) stu(F_RNG, rng.ctr);
         if (st == ST_SHADOW) {  // a closest query's ray travels in the query record
           stu(F_LIGHT, (uint32_t)light | ((uint32_t)ls << 16));
           if (ls > 0) stf(F_VIS, vis);
@@ -1192,6 +1137,100 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
   }
   // tell the host another step is needed: a plain store, no atomic (all writers store 1)
   if (__ballot(want) != 0ull && (threadIdx.x & 63) == 0) *a.any_query = 1u;
+}
+
+// New samples.  A slot-wave whose 64 slots are all idle (every sample of its batch finished,
+// or the slots are fresh) pulls the next batch of 64 consecutive units -- one pixel's
+// samples: coherent rays -- from its counter shard (one 128-B line per shard), and each
+// slot starts its sample: compute_pixel_color's jittered sub-position and the camera ray
+// (raytracer.cpp:18-70, camera.cpp:98-179), whose closest-hit query it emits.  Runs after
+// logic_kernel in every step (the same step in which a wave's last sample finishes), at
+// 8 waves per SIMD: the sample-start code kept in logic_kernel cost it 36 registers.
+__global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
+  const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
+  if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
+  const int N = a.n_slots;
+  uint32_t* S = a.state;
+  if (__ballot((int)S[F_UNIT * N + slot] != -2) != 0ull) return;  // some slot still works on its sample
+  const int lane = (int)(threadIdx.x & 63);
+  const int wave = slot >> 6;
+  const int shard = wave % a.batch_shards;
+  unsigned int j = 0;
+  if (lane == 0) j = atomicAdd(a.batch_ctr + shard * kCtrStride, 1u);
+  j = __shfl(j, 0);
+  const long long batch = (long long)j * a.batch_shards + shard;
+  const long long unit = batch * 64 + lane;
+  if (batch * 64 >= a.n_units) {  // every unit claimed: the slot-wave retires (n_units is a multiple of 64)
+    S[F_UNIT * N + slot] = 0xFFFFFFFFu;
+    if (lane == 0) a.wave_done[wave] = 1u;
+    return;
+  }
+  int px, py, sample;
+  if (!unit_coords(a, unit, px, py, sample)) return;  // edge tile: pixel outside the image (stays idle)
+  // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)
+  Rng rng;
+  rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
+  const int s = a.spp_sqrt;
+  float fx, fy;
+  if (s <= 1) {
+    fx = (float)px + 0.5f;
+    fy = (float)py + 0.5f;
+  } else {
+    int si = sample % s, sj = sample / s;
+    double ox = rng.next();
+    double oy = rng.next();
+    double sx = ((double)si + ox) / (double)s;
+    double sy = ((double)sj + oy) / (double)s;
+    fx = (float)((double)px + sx);
+    fy = (float)((double)py + sy);
+  }
+  Ray ray = camera_ray(a.cam, fx, fy, rng);
+  ray.time = (float)rng.next();
+  S[F_UNIT * N + slot] = (uint32_t)unit;
+  S[F_CTRL * N + slot] = (uint32_t)ST_CLOSEST;  // depth 0
+  if (a.late_draws) {
+    S[F_RNG * N + slot] = rng.ctr;
+    S[F_KEY * N + slot] = (uint32_t)rng.key;
+    S[(F_KEY + 1) * N + slot] = (uint32_t)(rng.key >> 32);
+  }
+  store_query(a.query, N, slot, ray.o, ray.d, ray.time, 0);
+  if (lane == __ffsll((long long)__ballot(1)) - 1) *a.any_query = 1u;
+}
+
+// The next soft-shadow sample of a light (shade, raytracer.cpp:214-236): a slot in ST_SHADOW
+// whose light (radius > 0) still has samples to draw after this result adds the result to its
+// visibility count and emits the next sample's shadow query -- the logic kernel's own ops
+// for that transition, in a kernel light enough to run at 8 waves per SIMD (the logic
+// kernel with recursion frames runs at 2).  It runs first in the step and marks the result
+// word it consumed (kResAdvanced); the logic kernel then leaves exactly those slots alone.
+__global__ __launch_bounds__(kBlock, 8) void shadow_step_kernel(LogicArgs a) {
+  const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
+  if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u || slot >= a.slot_end) return;
+  const int N = a.n_slots;
+  const uint32_t* S = a.state;
+  if ((int)S[F_UNIT * N + slot] < 0 || (S[F_CTRL * N + slot] & 15u) != (uint32_t)ST_SHADOW) return;
+  const uint32_t lw = S[F_LIGHT * N + slot];
+  const int light = (int)(lw & 0xffffu), ls = (int)(lw >> 16);
+  const rt_light& L = a.lights[light];
+  if (!(L.radius > 0.0f && ls + 1 < a.light_samples)) return;
+  float vis = ls > 0 ? __uint_as_float(S[F_VIS * N + slot]) : 0.0f;
+  if (a.result[slot] == 0) vis += 1.0f;
+  Rng rng;
+  rng.key = (uint64_t)S[F_KEY * N + slot] | ((uint64_t)S[(F_KEY + 1) * N + slot] << 32);
+  rng.ctr = S[F_RNG * N + slot];
+  const HitRec hr = load_hit(hit_rec(a.hit, slot));
+  V3 target{L.location[0], L.location[1], L.location[2]};
+  target = add(target, mul(rng.in_unit_sphere(), L.radius));
+  const V3 lv = sub(target, hr.p);
+  const float qtmax = sqrtf(dot(lv, lv));
+  const V3 qd = normalize(lv);
+  const V3 qo = add(hr.p, mul(hr.n, 1e-4f));
+  uint32_t* W = a.state;
+  W[F_LIGHT * N + slot] = (uint32_t)light | ((uint32_t)(ls + 1) << 16);
+  W[F_VIS * N + slot] = __float_as_uint(vis);
+  W[F_RNG * N + slot] = rng.ctr;
+  store_query(a.query, N, slot, qo, qd, qtmax, 1);
+  a.result[slot] = kResAdvanced;
 }
 
 // compute_pixel_color's accumulation (raytracer.cpp:46-69): totalColor starts at {0,0,0},
@@ -1368,6 +1407,7 @@ struct rt_scene_s {
   void* d_ref_boxes = nullptr;
   int n_cu = 0, trace_blocks_per_cu = 0;
   bool late_draws = false;  // a light with radius > 0 or a rough material: draws after a sample's start
+  bool soft_lights = false;  // a light with radius > 0 (several shadow samples with -light_sample > 1)
   int* d_spill = nullptr;
   size_t spill_cap = 0;
   // per-render workspace (grown on demand)
@@ -1494,7 +1534,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   rt_scene_s* s = new rt_scene_s();
   s->device = device;
   s->desc = *d;
-  for (int i = 0; i < d->n_lights; ++i) s->late_draws = s->late_draws || d->lights[i].radius > 0.0f;
+  for (int i = 0; i < d->n_lights; ++i) s->soft_lights = s->soft_lights || d->lights[i].radius > 0.0f;
+  s->late_draws = s->soft_lights;
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
   int rc = RT_OK;
   if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
@@ -1679,6 +1720,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.hit = s->d_hit;
   la.late_draws = s->late_draws ? 1 : 0;
   la.pinhole = cam->aperture <= 0.0f ? 1 : 0;
+  la.multi_shadow = s->soft_lights && p->light_samples > 1 ? 1 : 0;
+  if (const char* e = std::getenv("RT_SHADOW_STEP")) la.multi_shadow = la.multi_shadow && std::atoi(e) != 0;
   la.wave_done = s->d_wave_done;
   la.batch_ctr = s->d_batch_ctr;
   // every shard needs a slot-wave to drain it (wave w claims from shard w % batch_shards)
@@ -1793,7 +1836,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       for (int k = 0; k < batch; ++k) {
         // per-step reset: trace work counters + any_query (the line after them)
         HIP_TRY(hipMemsetAsync(P.ta.fetch, 0, ((size_t)ta.fetch_shards + 1) * kFetchStride * 4, P.st), RT_EDEVICE);
+        if (P.la.multi_shadow) {  // first: the logic kernel skips the slots it advanced
+          hipLaunchKernelGGL(shadow_step_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
+          HIP_TRY(hipGetLastError(), RT_EDEVICE);
+        }
         launch_logic(P.la, need_frames, tex, planes_only, P.logic_blocks, P.st);
+        HIP_TRY(hipGetLastError(), RT_EDEVICE);
+        hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipMemcpyAsync(flag + (size_t)k * kFetchStride, P.la.any_query, 4, hipMemcpyDeviceToHost, P.st),
                 RT_EDEVICE);

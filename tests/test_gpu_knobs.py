@@ -4,7 +4,8 @@ Each knob is read once per process (environment), so every configuration renders
 child process and must match the oracle bit for bit: the LDS traversal stack cut to 2
 entries (every deeper entry spills to HBM), extreme refill / leaf-phase thresholds, one and
 many work-counter shards, a slot count so small that a frame takes dozens of steps, and the
-slots split into two pipelines on two streams.
+slots split into two pipelines on two streams, and soft-shadow samples advanced by the logic
+kernel instead of shadow_step_kernel.
 """
 import os
 import subprocess
@@ -40,6 +41,7 @@ KNOBS = [
     {"RT_MAX_UNITS": "3000"},  # the call runs as many tile chunks
     {"RT_PIPES": "2"},  # two slot pipelines on two streams
     {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
+    {"RT_SHADOW_STEP": "0"},  # soft-shadow samples advanced by the logic kernel itself
 ]
 
 

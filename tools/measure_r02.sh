@@ -2,12 +2,15 @@
 # One GPU measurement pass (run on the GPU box through gpurun):
 #   bash tools/measure_r02.sh LABEL [skip-tests]
 # smoke + GPU parity tests, rocprofv3 kernel-trace stats of the headline bench, PMC passes
-# (FETCH_SIZE, WRITE_SIZE, VALU set; one pass each), then the full bench (with the CPU
-# baseline) carrying the PMC summaries just measured.  Everything lands in gpurun_out/.
+# (FETCH_SIZE, WRITE_SIZE, VALU set; one pass each), the full headline bench (with the CPU
+# baseline) carrying the PMC summaries just measured, then the other BASELINE configs (C2,
+# C3, C4), one rank's share of 2/4/8-way splits, and C5 (4096^2 x 64 spp) on one GPU.
+# Everything lands in gpurun_out/.
 set -eo pipefail
 L=${1:?label}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+B=tests/golden/scenes/blend
 if [ "${2:-}" != "skip-tests" ]; then
   echo "smoke $(date +%T)"
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${L}_smoke.log 2>&1
@@ -24,5 +27,14 @@ python3 tools/pmc_traffic.py --fetch gpurun_out/${L}_pmcF --write gpurun_out/${L
 python3 tools/pmc_valu.py --dir gpurun_out/${L}_pmcV --out gpurun_out/${L}_pmc_valu.json --label "$L" > /dev/null
 python3 tools/pmc_valu.py --dir gpurun_out/${L}_pmcV --kernel "logic_kernel" --out gpurun_out/${L}_pmc_valu_logic.json --label "$L" > /dev/null || true
 echo "bench $(date +%T)"
-timeout -k 10 600 python3 bench.py --pmc-traffic gpurun_out/${L}_pmc_traffic.json --pmc-valu gpurun_out/${L}_pmc_valu.json > gpurun_out/${L}_bench.json 2> gpurun_out/${L}_bench.err
+timeout -k 10 600 python3 bench.py --steps 10 --warmup 2 --pmc-traffic gpurun_out/${L}_pmc_traffic.json --pmc-valu gpurun_out/${L}_pmc_valu.json > gpurun_out/${L}_bench.json 2> gpurun_out/${L}_bench.err
+echo "configs $(date +%T)"
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --primary-only --spp-sqrt 1 > gpurun_out/${L}_c2_primary_only_bench.json 2> gpurun_out/${L}_c2.err
+timeout -k 10 300 python3 bench.py --steps 3 --scene $B/Antialiasing.json > gpurun_out/${L}_c3_antialiasing_bench.json 2> gpurun_out/${L}_c3.err
+timeout -k 10 300 python3 bench.py --steps 2 --scene $B/glossy_reflection.json --light-radius 1.0 --light-samples 4 > gpurun_out/${L}_c4_glossy_soft_bench.json 2> gpurun_out/${L}_c4.err
+for N in 2 4 8; do
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --emulate $N --emulate-rank $((N - 1)) > gpurun_out/${L}_emulated_share_of_${N}_bench.json 2> gpurun_out/${L}_em$N.err
+done
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --res 4096 --spp-sqrt 8 > gpurun_out/${L}_c5_4096_64spp_1gpu_bench.json 2> gpurun_out/${L}_c5.err
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --res 4096 --spp-sqrt 8 --emulate 8 --emulate-rank 3 > gpurun_out/${L}_c5_emulated_rank3_of_8_bench.json 2> gpurun_out/${L}_c5e.err
 echo "done $(date +%T)"
