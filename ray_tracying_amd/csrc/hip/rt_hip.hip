@@ -130,6 +130,7 @@ __device__ __forceinline__ void store_no_query(float* Q, int N, int slot) { Q[Q_
 enum FrField : int { FR_A = 0, FR_META = 3, FR_COUNT = 4 };
 
 enum : int { ST_SAMPLE = 0, ST_CLOSEST = 1, ST_SHADOW = 2 };
+constexpr unsigned int kWaveIdle = 2u;  // wave_done value: every slot of the wave idle (start_kernel's work)
 // result word of a shadow query that shadow_step_kernel consumed in this step (results are
 // otherwise >= -1: a primitive index, -1 for a miss, or 0 / 1 for a shadow query)
 constexpr int kResAdvanced = -2;
@@ -178,7 +179,8 @@ struct LogicArgs {
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   int multi_shadow;      // some light has radius > 0 and light_samples > 1: shadow_step_kernel runs first
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
-  unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it)
+  unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it);
+                            // kWaveIdle from logic_kernel to start_kernel: every slot is idle
 };
 
 struct TraceArgs {
@@ -1135,8 +1137,14 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
       }
     }
   }
-  // tell the host another step is needed: a plain store, no atomic (all writers store 1)
-  if (__ballot(want) != 0ull && (threadIdx.x & 63) == 0) *a.any_query = 1u;
+  // tell the host another step is needed: a plain store, no atomic (all writers store 1); a
+  // slot-wave left with no query (every sample of its batch finished) is flagged for
+  // start_kernel, which pulls its next batch in this same step
+  const bool wave_wants = __ballot(want) != 0ull;
+  if ((threadIdx.x & 63) == 0) {
+    if (wave_wants) *a.any_query = 1u;
+    else a.wave_done[slot >> 6] = kWaveIdle;
+  }
 }
 
 // New samples.  A slot-wave whose 64 slots are all idle (every sample of its batch finished,
@@ -1148,10 +1156,10 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
 // 8 waves per SIMD: the sample-start code kept in logic_kernel cost it 36 registers.
 __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
   const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
-  if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
+  // only the slot-waves logic_kernel flagged in this step (one scalar load per wave)
+  if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != kWaveIdle) return;
   const int N = a.n_slots;
   uint32_t* S = a.state;
-  if (__ballot((int)S[F_UNIT * N + slot] != -2) != 0ull) return;  // some slot still works on its sample
   const int lane = (int)(threadIdx.x & 63);
   const int wave = slot >> 6;
   const int shard = wave % a.batch_shards;
@@ -1165,6 +1173,7 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
     if (lane == 0) a.wave_done[wave] = 1u;
     return;
   }
+  if (lane == 0) a.wave_done[wave] = 0u;
   int px, py, sample;
   if (!unit_coords(a, unit, px, py, sample)) return;  // edge tile: pixel outside the image (stays idle)
   // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)

@@ -94,7 +94,7 @@ def test_cli_k1_matches_reference(tree, gpu):
     scenes.write(scenes.ascii((256, 256), roughness=0.0), str(tree / "ASCII" / "K1.json"))
     cwd = str(tree / "Code" / "build")
     rc, out, err = run(CLI, ["-input", "K1.json", "-bvh", "-s", "1", "-output", "k1.ppm"], cwd)
-    assert rc == 0, err
+    assert rc == 0, err[-3:]
     md5 = hashlib.md5((tree / "Output" / "k1.ppm").read_bytes()).hexdigest()
     assert md5 == man["known_answer"]["K1"]["md5"]
     assert out == ["BVH built. Mode: ON", "Rendering 256x256 with 1x1 samples and 1 light sampling points ...",
@@ -106,7 +106,7 @@ def test_cli_k1_matches_reference(tree, gpu):
         assert (tree / "Output" / "k1_ref.ppm").read_bytes() == (tree / "Output" / "k1.ppm").read_bytes()
     # default output name, the image-tile path on one device (-gpus 1 renders in one call)
     rc, _, err = run(CLI, ["-input", "K1.json", "-bvh", "-s", "1", "-gpus", "1"], cwd)
-    assert rc == 0, err
+    assert rc == 0, err[-3:]
     assert hashlib.md5((tree / "Output" / "output.ppm").read_bytes()).hexdigest() == md5
 
 
