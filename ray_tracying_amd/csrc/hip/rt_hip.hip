@@ -482,11 +482,21 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
+#ifdef RT_NODE_SOA
+  // A/B layout (make variant VDEFS=-DRT_NODE_SOA): the node's four 16-B words in four arrays
+  const float4* nd = a.c.nodes + node;
+  const size_t nn = (size_t)a.n_nodes;
+  const float4 g = nd[0];
+  const uint4 qa = *reinterpret_cast<const uint4*>(nd + nn);
+  const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2 * nn);
+  const int4 qc = *reinterpret_cast<const int4*>(nd + 3 * nn);
+#else
   const float4* nd = a.c.nodes + (size_t)node * 4;
   const float4 g = nd[0];
   const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
   const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
   const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
+#endif
   const uint32_t ex = __float_as_uint(g.w);
   const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
   const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
@@ -1484,6 +1494,19 @@ static int upload(void** dst, const void* src, size_t bytes) {
   return RT_OK;
 }
 
+// The 64-B nodes as laid out in HBM: AoS (one node = four consecutive 16-B words, fetched by
+// one lane), or -- the RT_NODE_SOA A/B build -- word k of every node in array k.
+static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
+#ifdef RT_NODE_SOA
+  std::vector<float4> t((size_t)n * 4);
+  for (int32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 4; ++k) std::memcpy(&t[(size_t)k * n + i], reinterpret_cast<const char*>(&nodes[i]) + 16 * k, 16);
+  return upload(dst, t.data(), t.size() * sizeof(float4));
+#else
+  return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
+#endif
+}
+
 int rt_scene_destroy(rt_scene_t s) {
   if (!s) return RT_OK;
   (void)hipSetDevice(s->device);
@@ -1548,7 +1571,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
   int rc = RT_OK;
   if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
-      (rc = upload(&s->d_nodes, d->nodes, (size_t)d->n_nodes * sizeof(rt_node4))) ||
+      (rc = upload_nodes(&s->d_nodes, d->nodes, d->n_nodes)) ||
       (rc = upload(&s->d_prim_refs, d->prim_refs, (size_t)d->n_prims * sizeof(rt_prim_ref))) ||
       (rc = upload(&s->d_ref_boxes, d->ref_leaf_boxes, (size_t)d->n_ref_leaves * 8 * sizeof(float))) ||
       (rc = upload(&s->d_mats, d->materials, (size_t)d->n_materials * sizeof(rt_material))) ||
