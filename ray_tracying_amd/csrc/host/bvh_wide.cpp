@@ -16,6 +16,9 @@
 //   * Sphere / Cube / Rectangle: the reference's own bbox (swept over time for moving spheres)
 //     + rounding margin.  Non-finite boxes (zero scale) -> unbounded list.
 #include <algorithm>
+#include <array>
+#include <functional>
+#include <string>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -758,7 +761,46 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
   for (int r : unbounded) new_order.push_back(r);  // the last n_unbounded, tested by every ray
   sc.n_unbounded = (int)unbounded.size();
 
-  // collapse BVH2 -> BVH4
+  // collapse BVH2 -> BVH4.  Default: SAH-optimal by dynamic programming over the BVH2
+  // (bottom-up: cost[i][k] = the least SAH cost of node i's subtree given k child slots of its
+  // parent -- one slot as a leaf or as a 4-wide node of its own, or split between its two
+  // children; the 4-wide node of BVH2 node i takes its children's best 4-slot split).
+  // RT_COLLAPSE=greedy: expand the largest-area internal child until four (round 1).
+  const bool dp_collapse = !(std::getenv("RT_COLLAPSE") && std::string(std::getenv("RT_COLLAPSE")) == "greedy");
+  const int n2 = (int)T.nodes.size();
+  std::vector<std::array<float, 5>> dpc(dp_collapse ? n2 : 0);     // cost by slots (1..4)
+  std::vector<std::array<uint8_t, 5>> dps(dp_collapse ? n2 : 0);   // 0: one slot; j: j slots to the left child
+  for (int i = (int)dpc.size() - 1; i >= 0; --i) {  // children follow their parent (DFS pre-order)
+    const Node2& nd = T.nodes[i];
+    const float A = area(nd.box);
+    if (nd.left < 0) {
+      for (int k = 1; k <= 4; ++k) { dpc[i][k] = A * (float)nd.count; dps[i][k] = 0; }
+      continue;
+    }
+    float dist[5] = {0, 0, 0, 0, 0};
+    uint8_t dj[5] = {0, 0, 0, 0, 0};
+    for (int k = 2; k <= 4; ++k) {
+      dist[k] = INFINITY;
+      for (int j = 1; j < k; ++j) {
+        const float c = dpc[nd.left][j] + dpc[nd.right][k - j];
+        if (c < dist[k]) { dist[k] = c; dj[k] = (uint8_t)j; }
+      }
+    }
+    dpc[i][1] = A * B.kNodeCost + dist[4];
+    dps[i][1] = 0;
+    for (int k = 2; k <= 4; ++k) {
+      if (dist[k] < dpc[i][1]) { dpc[i][k] = dist[k]; dps[i][k] = dj[k]; }
+      else { dpc[i][k] = dpc[i][1]; dps[i][k] = 0; }
+    }
+    dps[i][0] = dj[4];  // the 4-slot split of i's own children, used when i becomes a node
+  }
+  // the BVH2 nodes that become the child slots of the 4-wide node made from internal node n
+  std::function<void(int, int, std::vector<int>&)> gather = [&](int n, int k, std::vector<int>& out) {
+    const uint8_t j = dps[n][k];
+    if (k == 1 || j == 0) { out.push_back(n); return; }
+    gather(T.nodes[n].left, j, out);
+    gather(T.nodes[n].right, k - j, out);
+  };
   sc.node4.clear();
   sc.stack_bound = 1;
   if (!bounded.empty()) {
@@ -781,6 +823,10 @@ void build_wide(Scene& sc, const std::vector<Box>& shape_box, const std::vector<
       const Node2& root = T.nodes[it.n2];
       if (root.left < 0) {
         kids.push_back(it.n2);
+      } else if (dp_collapse) {
+        const int j = dps[it.n2][0];
+        gather(root.left, j, kids);
+        gather(root.right, 4 - j, kids);
       } else {
         kids = {root.left, root.right};
         while (kids.size() < 4) {

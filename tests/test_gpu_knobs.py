@@ -5,7 +5,8 @@ child process and must match the oracle bit for bit: the LDS traversal stack cut
 entries (every deeper entry spills to HBM), extreme refill / leaf-phase thresholds, one and
 many work-counter shards, a slot count so small that a frame takes dozens of steps, and the
 slots split into two pipelines on two streams, and soft-shadow samples advanced by the logic
-kernel instead of shadow_step_kernel.
+kernel instead of shadow_step_kernel, and the greedy BVH4 collapse instead of the
+SAH-optimal one.
 """
 import os
 import subprocess
@@ -42,6 +43,7 @@ KNOBS = [
     {"RT_PIPES": "2"},  # two slot pipelines on two streams
     {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
     {"RT_SHADOW_STEP": "0"},  # soft-shadow samples advanced by the logic kernel itself
+    {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
 ]
 
 
