@@ -1255,7 +1255,10 @@ __global__ __launch_bounds__(kBlock, 8) void shadow_step_kernel(LogicArgs a) {
 // compute_pixel_color's accumulation (raytracer.cpp:46-69): totalColor starts at {0,0,0},
 // adds every sample's Trace colour in (j, i) order, then divides by (float)(s*s); with
 // s <= 1 the single Trace colour is returned as is.
-constexpr int kRedChunk = 16;                  // samples per pixel staged per pass
+#ifndef RT_RED_CHUNK
+#define RT_RED_CHUNK 16
+#endif
+constexpr int kRedChunk = RT_RED_CHUNK;        // samples per pixel staged per pass (A/B: make variant)
 constexpr int kRedStride = kRedChunk * 3 + 1;  // padded LDS row (odd: conflict-free column reads)
 __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
   // The block's 256 pixels own a contiguous run of samples (unit = pixel * n_samples + s,
