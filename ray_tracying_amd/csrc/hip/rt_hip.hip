@@ -51,7 +51,8 @@ static int lds_stack_entries() {  // read per call: tests vary it within one pro
 }
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
-constexpr int kCtlBytes = 4096;    // control block; per-step reset region at byte 2048
+constexpr int kCtlBytes = 4096;    // control block (cleared by init_kernel)
+constexpr int kStatsBytes = 512;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
 // Batch-claim counters of the logic step: one per 128-B line (kCtrStride words apart) --
 // atomics on one line serialise at the memory side, so the shards must not share lines.
 constexpr int kMaxBatchShards = 1024;
@@ -63,7 +64,7 @@ constexpr int kMaxHostBatch = 16;
 // Slot pipelines: the slots are split into independent logic -> trace pipelines on their own
 // streams, so one pipeline's logic step and launch tail overlap the other's traversal.
 constexpr int kPipes = 2;
-constexpr size_t kFetchLines = (size_t)kMaxFetchShards + 1;  // fetch counters + any_query, per pipeline
+constexpr size_t kFetchLines = (size_t)kMaxFetchShards + 2;  // fetch counters + two any_query lines, per pipeline
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
 // field f of slot s lives at state[f * n_slots + s] (32-bit words; floats bit-cast)
@@ -179,6 +180,13 @@ struct LogicArgs {
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   int multi_shadow;      // some light has radius > 0 and light_samples > 1: shadow_step_kernel runs first
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
+  // per-step resets done by start_kernel's first block (no fill launches between kernels):
+  // the trace work counters of this step and the other any_query line (the next step's flag;
+  // the two lines alternate by step parity)
+  unsigned int* any_query_next;
+  unsigned int* fetch_reset;
+  int fetch_reset_n;
+  int first_step;        // the call's first step: slot-wave w takes batch w (no claim atomics)
   unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it);
                             // kWaveIdle from logic_kernel to start_kernel: every slot is idle
 };
@@ -194,6 +202,7 @@ struct TraceArgs {
   unsigned int* fetch;        // fetch_shards work counters over slot slices (zeroed per step)
   int fetch_shards;
   const unsigned int* any_query;  // logic's "some slot has a query" flag for this step
+  unsigned int* host_flag;    // pinned host word: any_query of this step, for the host's loop
   unsigned long long* rays;   // queries traced (one atomic per wave at exit)
   int n_slots;                // field stride of the per-slot arrays
   int slot_base, n_work;      // this pipeline's query slots: [slot_base, slot_base + n_work)
@@ -207,6 +216,9 @@ struct TraceArgs {
   int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
   int diag;                   // count_work under RT_DIAG: wave-level utilisation counters
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
+#ifdef RT_EXIT_TIMING
+  unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
+#endif
 };
 
 // ---------------------------------------------------------------- traversal
@@ -609,7 +621,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
   unsigned int nbox = 0, nprim = 0, nvisit = 0;
   unsigned long long dg_any_rays = 0, dg_any_box = 0;
   const TraceArgs& a = ta;
-  if (*ta.any_query == 0u) return;
+  const unsigned int any = *ta.any_query;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ta.host_flag = any;  // read by the host after the step
+  if (any == 0u) return;
   const unsigned nfs = (unsigned)ta.fetch_shards;
   const unsigned shard_len = (((nq + nfs - 1) / nfs) + 63u) & ~63u;
   // wave-uniform work queue: [q_next, q_end)
@@ -640,6 +654,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
     slot = -1;
   };
   RT_PT_DECL
+#ifdef RT_EXIT_TIMING
+  const unsigned long long et_begin = __builtin_amdgcn_s_memrealtime();
+  unsigned long long et_exh = 0;
+#endif
   for (;;) {
     RT_PT_MARK(3);  // loop control (ballots) since the node phase
     uint64_t act = __ballot(item != kNoItem);
@@ -667,6 +685,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
             }
             if (++sk >= (int)nfs) {
               exhausted = true;
+#ifdef RT_EXIT_TIMING
+              et_exh = __builtin_amdgcn_s_memrealtime();
+#endif
               break;
             }
           }
@@ -714,6 +735,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
 #endif
   }
   RT_PT_FLUSH
+#ifdef RT_EXIT_TIMING
+  if (lane == 0) {
+    unsigned long long* e = ta.exit_log + (size_t)(gtid >> 6) * 3;
+    e[0] = et_begin;
+    e[1] = et_exh;
+    e[2] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
 }
 
@@ -1166,6 +1195,10 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
 // 8 waves per SIMD: the sample-start code kept in logic_kernel cost it 36 registers.
 __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
   const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
+  if (blockIdx.x == 0) {  // this step's trace counters, and the next step's any_query line
+    for (int i = (int)threadIdx.x; i < a.fetch_reset_n; i += kBlock) a.fetch_reset[i * kFetchStride] = 0u;
+    if (threadIdx.x == 0) *a.any_query_next = 0u;
+  }
   // only the slot-waves logic_kernel flagged in this step (one scalar load per wave)
   if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != kWaveIdle) return;
   const int N = a.n_slots;
@@ -1174,8 +1207,12 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
   const int wave = slot >> 6;
   const int shard = wave % a.batch_shards;
   unsigned int j = 0;
-  if (lane == 0) j = atomicAdd(a.batch_ctr + shard * kCtrStride, 1u);
-  j = __shfl(j, 0);
+  if (a.first_step) {  // batch w for wave w: init_kernel set each shard's counter past them
+    j = (unsigned)(wave / a.batch_shards);
+  } else {
+    if (lane == 0) j = atomicAdd(a.batch_ctr + shard * kCtrStride, 1u);
+    j = __shfl(j, 0);
+  }
   const long long batch = (long long)j * a.batch_shards + shard;
   const long long unit = batch * 64 + lane;
   if (batch * 64 >= a.n_units) {  // every unit claimed: the slot-wave retires (n_units is a multiple of 64)
@@ -1325,16 +1362,42 @@ __global__ __launch_bounds__(kBlock) void quantise_kernel(const float* rgb, long
   out[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
-// slot initialisation: slot k takes unit k (units past the end retire immediately); a unit
-// whose pixel is outside the image (edge tiles) is skipped by the first logic step.
-__global__ __launch_bounds__(kBlock) void init_kernel(uint32_t* state, int n_slots, long long n_units, int* result,
-                                                      float* query, unsigned int* wave_done) {
+// Slot initialisation: every slot idle and every slot-wave flagged for start_kernel, which
+// starts the call's first step (there is nothing for logic_kernel to consume yet).  Block 0
+// also clears the control block and the pipelines' trace counters / any_query lines, and sets
+// each claim counter past the first-step batches (wave w takes batch w = j * shards + w %
+// shards, so shard k's counter starts at the number of waves w with w % shards == k).
+struct InitArgs {
+  uint32_t* state;
+  int n_slots;
+  int* result;
+  float* query;
+  unsigned int* wave_done;
+  unsigned int* ctl;
+  int ctl_words;
+  unsigned int* fetch;
+  int fetch_words;
+  unsigned int* batch_ctr;
+  int batch_shards;
+};
+__global__ __launch_bounds__(kBlock) void init_kernel(InitArgs a) {
   const int slot = blockIdx.x * kBlock + threadIdx.x;
-  if (slot >= n_slots) return;
+  if (blockIdx.x == 0) {
+    for (int i = (int)threadIdx.x; i < a.ctl_words; i += kBlock) a.ctl[i] = 0u;
+    for (int i = (int)threadIdx.x; i < a.fetch_words; i += kBlock) a.fetch[i] = 0u;
+    const int waves = a.n_slots >> 6;
+    for (int k = (int)threadIdx.x; k < a.batch_shards; k += kBlock)
+      a.batch_ctr[k * kCtrStride] = (unsigned)(waves / a.batch_shards + (k < waves % a.batch_shards ? 1 : 0));
+  }
+  if (slot >= a.n_slots) return;
+  const int n_slots = a.n_slots;
+  uint32_t* state = a.state;
   // only the control words: every other field is written by the logic step before it is read
   // (slots are reused sample after sample without clearing, so nothing may rely on zeros)
-  state[F_UNIT * n_slots + slot] = (uint32_t)-2;  // idle: the first logic step pulls a batch
-  if ((slot & 63) == 0) wave_done[slot >> 6] = 0u;
+  state[F_UNIT * n_slots + slot] = (uint32_t)-2;  // idle: start_kernel pulls a batch
+  if ((slot & 63) == 0) a.wave_done[slot >> 6] = kWaveIdle;
+  int* result = a.result;
+  float* query = a.query;
   state[F_CTRL * n_slots + slot] = ST_SAMPLE;
   result[slot] = -1;
   store_no_query(query, n_slots, slot);
@@ -1365,7 +1428,7 @@ static int fetch_shards_env() {
 static int batch_shards_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_BATCH_SHARDS");
-    return e ? std::max(1, std::min(kMaxBatchShards, std::atoi(e))) : 32;
+    return e ? std::max(1, std::min(kMaxBatchShards, std::atoi(e))) : 128;
   }();
   return v;
 }
@@ -1433,8 +1496,7 @@ struct rt_scene_s {
   int* d_spill = nullptr;
   size_t spill_cap = 0;
   // per-render workspace (grown on demand)
-  void* d_ctl = nullptr;  // bytes 16/24: box/prim tests, 32: rays (u64), 2048: trace work counters, 3072: any_query,
-                          // batch-claim counters: d_batch_ctr
+  void* d_ctl = nullptr;  // bytes 16/24: box/prim tests, 32: rays (u64), 240..: diagnostics, 488: node visits
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
   uint32_t* d_state = nullptr;
@@ -1448,6 +1510,8 @@ struct rt_scene_s {
   unsigned int* d_wave_done = nullptr;
   size_t slots_cap = 0;
   unsigned int* h_flag = nullptr;  // pinned: per pipeline, one 128-B line per step of a host batch (any_query copies)
+  unsigned long long* h_stats = nullptr;  // pinned: the first kStatsBytes of the control block, copied after each batch
+  std::vector<int32_t> tiles_on_device;   // the tile list d_tiles holds
   unsigned int* d_batch_ctr = nullptr;  // kMaxBatchShards counters, one 128-B line each
   unsigned int* d_fetch = nullptr;      // per pipeline: trace fetch counters (one line each) + any_query line
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr, ev_fork = nullptr, ev_join = nullptr;
@@ -1520,6 +1584,7 @@ int rt_scene_destroy(rt_scene_t s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
+  if (s->h_stats) (void)hipHostFree(s->h_stats);
   hipEvent_t evs[] = {s->ev_t0, s->ev_t1, s->ev_fork, s->ev_join};
   for (hipEvent_t e : evs)
     if (e) (void)hipEventDestroy(e);
@@ -1592,6 +1657,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   }
   if (!ev_ok || hipMalloc(&s->d_ctl, kCtlBytes) != hipSuccess ||
       hipHostMalloc((void**)&s->h_flag, (size_t)kPipes * kMaxHostBatch * kFetchStride * 4) != hipSuccess ||
+      hipHostMalloc((void**)&s->h_stats, kStatsBytes) != hipSuccess ||
       hipMalloc(&s->d_batch_ctr, (size_t)kMaxBatchShards * kCtrStride * 4) != hipSuccess ||
       hipMalloc(&s->d_fetch, (size_t)kPipes * kFetchLines * kFetchStride * 4) != hipSuccess ||
       hipEventCreate(&s->ev_t0) != hipSuccess || hipEventCreate(&s->ev_t1) != hipSuccess ||
@@ -1687,6 +1753,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     s->d_tiles = nullptr;
     s->tiles_cap = 0;
+    s->tiles_on_device.clear();
     HIP_TRY(hipMalloc(&s->d_tiles, (size_t)n_tiles * sizeof(int32_t)), RT_ENOMEM);
     s->tiles_cap = (size_t)n_tiles;
   }
@@ -1709,9 +1776,14 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_samples, (size_t)n_units * 3 * sizeof(float)), RT_ENOMEM);
     s->samples_cap = (size_t)n_units * 3;
   }
-  HIP_TRY(hipMemcpyAsync(s->d_tiles, tile_ids, (size_t)n_tiles * sizeof(int32_t), hipMemcpyHostToDevice, stream), RT_EDEVICE);
-  unsigned int* ctl = (unsigned int*)s->d_ctl;
-  HIP_TRY(hipMemsetAsync(ctl, 0, kCtlBytes, stream), RT_EDEVICE);
+  // the tile list is uploaded only when it changed (a renderer's frames reuse one list)
+  if (s->tiles_on_device.size() != (size_t)n_tiles ||
+      !std::equal(tile_ids, tile_ids + n_tiles, s->tiles_on_device.begin())) {
+    s->tiles_on_device.assign(tile_ids, tile_ids + n_tiles);
+    HIP_TRY(hipMemcpyAsync(s->d_tiles, s->tiles_on_device.data(), (size_t)n_tiles * sizeof(int32_t),
+                           hipMemcpyHostToDevice, stream), RT_EDEVICE);
+  }
+  unsigned int* ctl = (unsigned int*)s->d_ctl;  // cleared by init_kernel
 
   LogicArgs la{};
   Common c{};
@@ -1760,8 +1832,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.wave_done = s->d_wave_done;
   la.batch_ctr = s->d_batch_ctr;
   // every shard needs a slot-wave to drain it (wave w claims from shard w % batch_shards)
-  la.batch_shards = std::max(1, std::min(batch_shards_env(), n_slots / 64));
-  HIP_TRY(hipMemsetAsync(s->d_batch_ctr, 0, (size_t)la.batch_shards * kCtrStride * 4, stream), RT_EDEVICE);
+  la.batch_shards = std::max(1, std::min(batch_shards_env(), n_slots / 64));  // counters set by init_kernel
 
   TraceArgs ta{};
   ta.c = c;
@@ -1790,7 +1861,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
   if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
   // the diagnostics wait on every step (one pipeline)
+#ifdef RT_EXIT_TIMING
+  const bool step_sync = true;
+#else
   const bool step_sync = diag || replay_iter >= 0;
+#endif
 
   // ---- pipelines: the slots may split into kPipes independent logic -> trace sequences, one
   // per stream (units are claimed from the shared batch counters, so the split changes no
@@ -1806,7 +1881,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     TraceArgs ta;
     hipStream_t st;
     unsigned logic_blocks, trace_blocks;
-    int iters;
+    int iters, steps;
     bool done;
   } pipes[kPipes];
   const int per_pipe = (n_slots / kBlock / n_pipes) * kBlock;
@@ -1824,13 +1899,14 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     P.ta.slot_base = base;
     P.ta.n_work = count;
     P.ta.fetch = s->d_fetch + (size_t)h * kFetchLines * kFetchStride;
-    P.la.any_query = P.ta.fetch + (size_t)ta.fetch_shards * kFetchStride;  // the line after the fetch counters
-    P.ta.any_query = P.la.any_query;
+    P.la.fetch_reset = P.ta.fetch;
+    P.la.fetch_reset_n = ta.fetch_shards;
     P.logic_blocks = (unsigned)(count / kBlock);
     P.trace_blocks = std::min(grid_cap, (unsigned)((count + kBlock - 1) / kBlock));
     P.ta.n_threads = (int)P.trace_blocks * kBlock;
     spill_need += (size_t)spill_entries * P.ta.n_threads;
     P.iters = 0;
+    P.steps = 0;
     P.done = false;
   }
   if (spill_need > s->spill_cap) {
@@ -1844,11 +1920,29 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     pipes[h].ta.spill = s->d_spill + (size_t)2 * off;
     off += spill_entries * pipes[h].ta.n_threads;
   }
+#ifdef RT_EXIT_TIMING
+  static unsigned long long* exit_log = nullptr;
+  if (!exit_log) HIP_TRY(hipMalloc(&exit_log, (size_t)1 << 22), RT_ENOMEM);  // 512 K u64: 170 K waves
+  for (int h = 0; h < n_pipes; ++h) pipes[h].ta.exit_log = exit_log;
+#endif
 
   const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, s->d_state, n_slots, n_units, s->d_result,
-                     s->d_query, s->d_wave_done);
-  HIP_TRY(hipGetLastError(), RT_EDEVICE);
+  {
+    InitArgs ia{};
+    ia.state = s->d_state;
+    ia.n_slots = n_slots;
+    ia.result = s->d_result;
+    ia.query = s->d_query;
+    ia.wave_done = s->d_wave_done;
+    ia.ctl = ctl;
+    ia.ctl_words = kCtlBytes / 4;
+    ia.fetch = s->d_fetch;
+    ia.fetch_words = (int)(kPipes * kFetchLines * kFetchStride);
+    ia.batch_ctr = s->d_batch_ctr;
+    ia.batch_shards = la.batch_shards;
+    hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, ia);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+  }
 
   // ---- iterate logic -> trace per pipeline until none of its slots issues a query
   double trace_ms = 0.0;
@@ -1863,35 +1957,55 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     for (int h = 1; h < n_pipes; ++h) HIP_TRY(hipStreamWaitEvent(pipes[h].st, s->ev_fork, 0), RT_EDEVICE);
   }
   const bool tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
+  // Each host batch ends with the reduce and the statistics copy, so the wait for its last
+  // event covers the frame when the batch was long enough (the usual case: it is sized by the
+  // previous call); otherwise more steps follow and the reduce runs again.
+  unsigned long long* h_stats = s->h_stats;
   for (int live = n_pipes; live > 0;) {
     for (int h = 0; h < n_pipes; ++h) {
       Pipe& P = pipes[h];
       if (P.done) continue;
       unsigned int* flag = s->h_flag + (size_t)h * kMaxHostBatch * kFetchStride;
       for (int k = 0; k < batch; ++k) {
-        // per-step reset: trace work counters + any_query (the line after them)
-        HIP_TRY(hipMemsetAsync(P.ta.fetch, 0, ((size_t)ta.fetch_shards + 1) * kFetchStride * 4, P.st), RT_EDEVICE);
-        if (P.la.multi_shadow) {  // first: the logic kernel skips the slots it advanced
-          hipLaunchKernelGGL(shadow_step_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
+        const int step = P.steps++;
+        // any_query lines alternate by step parity (start_kernel clears the next step's)
+        unsigned int* aq = P.ta.fetch + ((size_t)ta.fetch_shards + (step & 1)) * kFetchStride;
+        unsigned int* aq_next = P.ta.fetch + ((size_t)ta.fetch_shards + ((step + 1) & 1)) * kFetchStride;
+        P.la.any_query = aq;
+        P.la.any_query_next = aq_next;
+        P.la.first_step = step == 0 ? 1 : 0;
+        P.ta.any_query = aq;
+        P.ta.host_flag = flag + (size_t)k * kFetchStride;
+        if (step > 0) {  // the first step has no result to consume: start_kernel alone
+          if (P.la.multi_shadow) {  // first: the logic kernel skips the slots it advanced
+            hipLaunchKernelGGL(shadow_step_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
+            HIP_TRY(hipGetLastError(), RT_EDEVICE);
+          }
+          launch_logic(P.la, need_frames, tex, planes_only, P.logic_blocks, P.st);
           HIP_TRY(hipGetLastError(), RT_EDEVICE);
         }
-        launch_logic(P.la, need_frames, tex, planes_only, P.logic_blocks, P.st);
-        HIP_TRY(hipGetLastError(), RT_EDEVICE);
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
-        HIP_TRY(hipMemcpyAsync(flag + (size_t)k * kFetchStride, P.la.any_query, 4, hipMemcpyDeviceToHost, P.st),
-                RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
         launch_trace(P.ta, p->count_work != 0, planes_only, P.trace_blocks, lds, P.st);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
       }
     }
+    for (int h = 1; h < n_pipes; ++h) {  // the reduce waits for every pipeline's steps
+      if (pipes[h].done) continue;
+      HIP_TRY(hipEventRecord(s->ev_join, pipes[h].st), RT_EDEVICE);
+      HIP_TRY(hipStreamWaitEvent(stream, s->ev_join, 0), RT_EDEVICE);
+    }
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    if (stats) HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
+    HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
     for (int h = 0; h < n_pipes; ++h) {
       Pipe& P = pipes[h];
       if (P.done) continue;
       const unsigned int* flag = s->h_flag + (size_t)h * kMaxHostBatch * kFetchStride;
-      HIP_TRY(hipEventSynchronize(s->ev_b[h][batch - 1]), RT_EDEVICE);
       for (int k = 0; k < batch && !P.done; ++k) {
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[h][k], s->ev_b[h][k]), RT_EDEVICE);
@@ -1919,6 +2033,24 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
                        (rays1 - rays0) / (unsigned long long)replay_reps, tot / replay_reps, best, replay_reps);
         }
         const bool more = flag[(size_t)k * kFetchStride] != 0;
+#ifdef RT_EXIT_TIMING
+        if (more) {  // wave start / queue-exhausted / exit times of this launch (100 MHz clock)
+          const int nw = (int)P.ta.n_threads / 64;
+          std::vector<unsigned long long> lg((size_t)nw * 3);
+          HIP_TRY(hipMemcpy(lg.data(), P.ta.exit_log, lg.size() * 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+          unsigned long long b0 = ~0ull, x0 = ~0ull;
+          std::vector<double> ex;
+          for (int w = 0; w < nw; ++w) {
+            b0 = std::min(b0, lg[(size_t)w * 3]);
+            if (lg[(size_t)w * 3 + 1]) x0 = std::min(x0, lg[(size_t)w * 3 + 1]);
+          }
+          for (int w = 0; w < nw; ++w) ex.push_back((double)(lg[(size_t)w * 3 + 2] - b0) * 1e-5);  // ms
+          std::sort(ex.begin(), ex.end());
+          std::fprintf(stderr, "[rt exit] step %2d: trace %.3f ms; queue exhausted at %.3f ms; waves exit: 10%% %.3f, 50%% %.3f, 90%% %.3f, 99%% %.3f, last %.3f ms\n",
+                       iters, ms, x0 == ~0ull ? -1.0 : (double)(x0 - b0) * 1e-5, ex[nw / 10], ex[nw / 2], ex[nw * 9 / 10],
+                       ex[nw * 99 / 100], ex[nw - 1]);
+        }
+#endif
         if (diag && more) {
           unsigned long long rc = 0;
           HIP_TRY(hipMemcpy(&rc, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
@@ -1938,21 +2070,10 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     }
     batch = step_sync ? 1 : 4;  // the previous render's count fell short: top up in small batches
   }
-  if (n_pipes > 1) {  // reduce after every pipeline's last step
-    for (int h = 1; h < n_pipes; ++h) {
-      HIP_TRY(hipEventRecord(s->ev_join, pipes[h].st), RT_EDEVICE);
-      HIP_TRY(hipStreamWaitEvent(stream, s->ev_join, 0), RT_EDEVICE);
-    }
-  }
   s->last_iters = 0;
   for (int h = 0; h < n_pipes; ++h) s->last_iters = std::max(s->last_iters, pipes[h].iters);
-  hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
-  HIP_TRY(hipGetLastError(), RT_EDEVICE);
-  HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
-  HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
   if (stats) {
-    unsigned long long cnt[3] = {0, 0, 0};
-    HIP_TRY(hipMemcpy(cnt, ctl + 4, sizeof(cnt), hipMemcpyDeviceToHost), RT_EDEVICE);
+    const unsigned long long* cnt = h_stats + 2;  // ctl bytes 16, 24, 32
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1), RT_EDEVICE);
     stats->rays = cnt[2];
@@ -1971,11 +2092,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     }
 #endif
     stats->node_visits = 0;
-    if (p->count_work) {  // lane-level node visits (trace_counters_out, ctl byte 488)
-      unsigned long long nv = 0;
-      HIP_TRY(hipMemcpy(&nv, ctl + 122, sizeof(nv), hipMemcpyDeviceToHost), RT_EDEVICE);
-      stats->node_visits = nv;
-    }
+    if (p->count_work) stats->node_visits = h_stats[61];  // lane-level node visits (trace_counters_out, ctl byte 488)
     if (p->count_work && std::getenv("RT_DIAG")) {
       unsigned long long dg[2] = {0, 0};
       HIP_TRY(hipMemcpy(dg, ctl + 128, sizeof(dg), hipMemcpyDeviceToHost), RT_EDEVICE);
