@@ -187,6 +187,8 @@ struct LogicArgs {
   unsigned int* fetch_reset;
   int fetch_reset_n;
   int first_step;        // the call's first step: slot-wave w takes batch w (no claim atomics)
+  int n_fuse;            // > 0: every closest hit's point-light shadow rays were traced with it (occl bits)
+  const unsigned int* occl;
   unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it);
                             // kWaveIdle from logic_kernel to start_kernel: every slot is idle
 };
@@ -215,6 +217,11 @@ struct TraceArgs {
   int refill_min;             // refill kernel: refill finished lanes when fewer than this many traverse
   int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
   int diag;                   // count_work under RT_DIAG: wave-level utilisation counters
+  // fused shadow rays (kFuse launches): point lights whose shadow rays a closest hit's lane
+  // traces right after the hit, and the per-slot occlusion bits it leaves for the logic step
+  const rt_light* lights;
+  int n_fuse;
+  unsigned int* occl;
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
@@ -610,7 +617,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 4  // waves per SIMD the register allocation targets (A/B builds: make variant)
 #endif
-template <bool kCount, bool kPlanesOnly>
+template <bool kCount, bool kPlanesOnly, bool kFuse>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_work;
@@ -648,10 +655,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
     if (a.c.n_prims > 0 && !a.c.use_bvh)
       test_prims<kCount, kPlanesOnly>(a, slot, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
   };
-  // the lane's query is complete: write it back and free the lane
+  // kFuse: 0 while the lane traces the slot's own query; (occlusion bits << 8) | (light + 1)
+  // while it traces the shadow ray of a point light for the closest hit it just found
+  int fz = 0;
+  // shade's shadow ray towards point light l from the slot's hit (raytracer.cpp:214-236; the
+  // logic step's ops for it, on the hit record this kernel stored)
+  auto fused_shadow = [&](int l) {
+    const HitRec hr = load_hit(hit_rec(a.hit, slot));
+    const rt_light& L = a.lights[l];
+    const V3 lv = sub(V3{L.location[0], L.location[1], L.location[2]}, hr.p);
+    const float tmax = sqrtf(dot(lv, lv));
+    setup_query(q, add(hr.p, mul(hr.n, 1e-4f)), normalize(lv), tmax, true);
+    ++nrays;
+    if (kCount) ++dg_any_rays;
+    start_traversal();
+  };
+  // the lane's query is complete: write it back and free the lane (kFuse: a closest hit goes
+  // on to its lights' shadow rays first; their occlusion bits are written after the last)
   auto settle = [&]() {
-    finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
-    slot = -1;
+    int next = -1;  // kFuse: the light whose shadow ray the lane traces next
+    if (kFuse && fz != 0) {
+      complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+      const int l = (fz & 0xff) - 1;
+      const unsigned bits = ((unsigned)fz >> 8) | (h.done ? 1u << l : 0u);
+      if (l + 1 < a.n_fuse) {
+        fz = (int)(bits << 8) | (l + 2);
+        next = l + 1;
+      } else {
+        a.occl[slot] = bits;
+        fz = 0;
+      }
+    } else {
+      finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+      if (kFuse && !q.any && h.best_idx >= 0) {
+        fz = 1;
+        next = 0;
+      }
+    }
+    if (kFuse && next >= 0) fused_shadow(next);
+    else slot = -1;
   };
   RT_PT_DECL
 #ifdef RT_EXIT_TIMING
@@ -952,6 +994,9 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
         rng.ctr = rng_ctr;
       }
       bool idle = st0 < 0;  // idle (batch done, pixel outside the image): start_kernel's work
+      // a closest hit whose point-light shadow rays the trace kernel traced along (kFuse)
+      const bool fused = a.n_fuse > 0 && st0 == ST_CLOSEST && res >= 0;
+      const unsigned occl_bits = fused ? a.occl[slot] : 0u;
       V3 qo{0, 0, 0}, qd{0, 0, 0};
       float qtmax = 0.0f;
       int qkind = 0;
@@ -989,6 +1034,11 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
             const rt_light& L = a.lights[light];
             const int ns = (L.radius > 0.0f) ? a.light_samples : 1;
             if (ls < ns) {
+              if (fused) {  // the trace kernel traced this shadow ray with the hit (result in occl bits)
+                if (!((occl_bits >> light) & 1u)) vis += 1.0f;
+                ++ls;
+                continue;
+              }
               V3 target{L.location[0], L.location[1], L.location[2]};
               if (L.radius > 0.0f) target = add(target, mul(rng.in_unit_sphere(), L.radius));
               V3 lv = sub(target, hp);
@@ -1410,12 +1460,15 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
 }
 // trace launch (the refill kernel; count: the instrumented variant)
 void launch_trace(const TraceArgs& ta, bool count, bool planes, unsigned blocks, size_t lds, hipStream_t st) {
+  const bool fuse = ta.n_fuse > 0;  // planes-only scenes only (the host's choice)
   if (count) {
-    if (planes) hipLaunchKernelGGL((trace_refill_kernel<true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    else hipLaunchKernelGGL((trace_refill_kernel<true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    if (fuse) hipLaunchKernelGGL((trace_refill_kernel<true, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    else if (planes) hipLaunchKernelGGL((trace_refill_kernel<true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    else hipLaunchKernelGGL((trace_refill_kernel<true, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   } else {
-    if (planes) hipLaunchKernelGGL((trace_refill_kernel<false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    else hipLaunchKernelGGL((trace_refill_kernel<false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    if (fuse) hipLaunchKernelGGL((trace_refill_kernel<false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    else if (planes) hipLaunchKernelGGL((trace_refill_kernel<false, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    else hipLaunchKernelGGL((trace_refill_kernel<false, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   }
 }
 static int fetch_shards_env() {
@@ -1507,6 +1560,7 @@ struct rt_scene_s {
   size_t samples_cap = 0;
   int* d_result = nullptr;
   float* d_hit = nullptr;
+  unsigned int* d_occl = nullptr;  // per slot: occlusion bits of fused shadow rays
   unsigned int* d_wave_done = nullptr;
   size_t slots_cap = 0;
   unsigned int* h_flag = nullptr;  // pinned: per pipeline, one 128-B line per step of a host batch (any_query copies)
@@ -1519,13 +1573,16 @@ struct rt_scene_s {
   hipEvent_t ev_a[kPipes][kMaxHostBatch] = {}, ev_b[kPipes][kMaxHostBatch] = {};
   hipStream_t aux[kPipes] = {};  // pipelines 1.. run on these non-blocking streams (0: the caller's)
   int last_iters = 0;  // steps the previous render took: the size of the next render's first host batch
+  int fuse_lights = 0;  // > 0: point lights whose shadow rays the trace kernel may fuse (see rt_scene_create)
 };
 
 static void free_workspace(rt_scene_s* s) {
-  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples, s->d_hit, s->d_wave_done};
+  void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples, s->d_hit, s->d_wave_done,
+                  s->d_occl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s->d_wave_done = nullptr;
+  s->d_occl = nullptr;
   s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
   s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr; s->d_hit = nullptr;
   s->slots_cap = 0;
@@ -1635,6 +1692,9 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   s->device = device;
   s->desc = *d;
   for (int i = 0; i < d->n_lights; ++i) s->soft_lights = s->soft_lights || d->lights[i].radius > 0.0f;
+  // fused shadow rays: planes-only scenes whose lights are all points (one shadow ray each,
+  // no random draws), at most 24 of them (occlusion bits of one word)
+  s->fuse_lights = d->prim_stride == 64 && !s->soft_lights && d->n_lights >= 1 && d->n_lights <= 24 ? d->n_lights : 0;
   s->late_draws = s->soft_lights;
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
   int rc = RT_OK;
@@ -1671,7 +1731,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const int lds_entries = std::min(d->stack_bound, lds_stack_entries());
     const bool planes = d->prim_stride == 64;
-    const void* fn = planes ? (const void*)trace_refill_kernel<false, true> : (const void*)trace_refill_kernel<false, false>;
+    const void* fn = planes ? (const void*)trace_refill_kernel<false, true, false> : (const void*)trace_refill_kernel<false, false, false>;
     const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kBlock, lds_bytes) != hipSuccess || bpc < 1)
       bpc = 2;
@@ -1764,6 +1824,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_hit, N * HIT_STRIDE * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_occl, N * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_wave_done, (N / 64 + 1) * 4), RT_ENOMEM);
     if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
     if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
@@ -1853,6 +1914,17 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.refill_min = refill_min_env();
   ta.leaf_min = leaf_min_env();
   ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
+  ta.lights = (const rt_light*)s->d_lights;
+  // Fused shadow rays pay when the call is small (at most two slot loads of samples: one
+  // rank's share of a split frame): each launch ends in a drain of ~0.45 ms that is the same
+  // for any launch size, and fusing halves the launches.  On a whole frame the lanes' camera
+  // and shadow rays then interleave within a wave and lose coherence (headline -6.5 %).
+  // RT_FUSE=0 / 1 overrides (1: whenever the scene allows it).
+  ta.n_fuse = n_units <= 2LL * n_slots ? s->fuse_lights : 0;
+  if (const char* e = std::getenv("RT_FUSE")) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
+  ta.occl = s->d_occl;
+  la.n_fuse = ta.n_fuse;
+  la.occl = s->d_occl;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
   // entry + t_near per stack slot
   const size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);

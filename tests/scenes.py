@@ -123,6 +123,25 @@ def soup(n=200, seed=5, res=(48, 48), light=True) -> dict:
     }
 
 
+def planes_lit(n=400, seed=17, res=(40, 32), n_lights=3) -> dict:
+    """A planes-only scene (the trace kernel's fused shadow-ray case) with point lights only:
+    a soup whose triangles cycle through a mirror, a glass (refraction, total internal
+    reflection), a glossy (random fuzz draws after the shadow rays) and a plain diffuse
+    material, lit by `n_lights` point lights around and inside the soup."""
+    sc = soup(n, seed=seed, res=res)
+    mats = [{"diffuse_color": [0.9, 0.9, 0.9], "reflectivity": 0.9, "roughness": 0.0, "k_ambient": 0.05},
+            {"diffuse_color": [0.8, 0.9, 1.0], "transparency": 0.85, "refractive_index": 1.5, "reflectivity": 0.1},
+            {"diffuse_color": [0.2, 0.4, 0.9], "reflectivity": 0.4, "roughness": 0.3},
+            {"diffuse_color": [0.9, 0.3, 0.2]}]
+    for k, pl in enumerate(sc["planes"]):
+        pl["material"] = dict(mats[k % len(mats)])
+    rnd = random.Random(seed + 1)
+    sc["lights"] = [{"location": [rnd.uniform(-2.5, 2.5), rnd.uniform(-3.5, 1.5), rnd.uniform(-2.5, 2.5)],
+                     "intensity": 200.0 + 20.0 * i, "color": [1.0, 0.9 - 0.01 * i, 0.8], "radius": 0.0}
+                    for i in range(n_lights)]
+    return sc
+
+
 def soup_degenerate(n=300, seed=13, res=(48, 48), every=7) -> dict:
     """A soup in which every `every`-th plane repeats its third corner (c3 == c2): the
     reference's trap (shapes.cpp:485-494) -- the degenerate sub-triangle

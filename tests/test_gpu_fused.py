@@ -1,0 +1,56 @@
+"""Fused shadow rays (trace_refill_kernel<.., kFuse>): in a planes-only scene lit by point
+lights only, the lane that finds a closest hit traces its lights' shadow rays right after it
+and leaves occlusion bits for the logic step.  Fused and unfused renders must both match the
+oracle bit for bit (and in ray count): with reflection, refraction and glossy fuzz after the
+shade (raytracer.cpp:180-350), in BVH and linear modes, and with 24 lights (the last bit of the
+occlusion word).  RT_FUSE is read per call, so each setting renders in a child process like
+the other knobs (tests/test_gpu_knobs.py)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import scenes
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import ray_tracying_amd as rt
+sc = rt.Scene(sys.argv[2])
+img, st = sc.render(rt.RenderParams(spp_sqrt=int(sys.argv[4]), light_samples=1, use_bvh=sys.argv[5] == "1", seed=9))
+np.save(sys.argv[3], img)
+print(st.rays)
+"""
+
+
+def render_child(path, out, spp, bvh, fuse):
+    r = subprocess.run([sys.executable, "-c", CHILD, ROOT, path, out, str(spp), "1" if bvh else "0"],
+                       env={**os.environ, "RT_FUSE": fuse}, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return np.load(out), int(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("bvh", [True, False])
+def test_fused_shadows_match_oracle(tmp_path, gpu, bvh):
+    p = scenes.write(scenes.planes_lit(), str(tmp_path / "p.json"))
+    ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=9, spp_sqrt=2, light_samples=1, use_bvh=bvh)
+    for fuse in ("1", "0"):
+        img, rays = render_child(p, str(tmp_path / f"img{fuse}.npy"), 2, bvh, fuse)
+        diff = int((img.view(np.uint32) != ref.view(np.uint32)).sum())
+        assert diff == 0, f"RT_FUSE={fuse}: {diff} channels differ"
+        assert rays == ost["rays"], fuse
+
+
+def test_fused_24_lights(tmp_path, gpu):
+    p = scenes.write(scenes.planes_lit(n=150, res=(24, 16), n_lights=24), str(tmp_path / "p24.json"))
+    ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=9, spp_sqrt=1, light_samples=1, use_bvh=True)
+    img, rays = render_child(p, str(tmp_path / "img.npy"), 1, True, "1")
+    assert int((img.view(np.uint32) != ref.view(np.uint32)).sum()) == 0
+    assert rays == ost["rays"]

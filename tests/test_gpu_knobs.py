@@ -6,7 +6,7 @@ entries (every deeper entry spills to HBM), extreme refill / leaf-phase threshol
 many work-counter shards, a slot count so small that a frame takes dozens of steps, and the
 slots split into two pipelines on two streams, and soft-shadow samples advanced by the logic
 kernel instead of shadow_step_kernel, and the greedy BVH4 collapse instead of the
-SAH-optimal one.
+SAH-optimal one, and point-light shadow rays left unfused in a small call.
 """
 import os
 import subprocess
@@ -44,6 +44,7 @@ KNOBS = [
     {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
     {"RT_SHADOW_STEP": "0"},  # soft-shadow samples advanced by the logic kernel itself
     {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
+    {"RT_FUSE": "0"},  # point-light shadow rays as their own queries (small calls fuse them by default)
 ]
 
 
