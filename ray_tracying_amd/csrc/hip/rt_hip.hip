@@ -2029,10 +2029,24 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     for (int h = 1; h < n_pipes; ++h) HIP_TRY(hipStreamWaitEvent(pipes[h].st, s->ev_fork, 0), RT_EDEVICE);
   }
   const bool tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
-  // Each host batch ends with the reduce and the statistics copy, so the wait for its last
-  // event covers the frame when the batch was long enough (the usual case: it is sized by the
-  // previous call); otherwise more steps follow and the reduce runs again.
+  // A host batch that should complete the call (by the previous call's step count) ends with
+  // the reduce and the statistics copy, so the host waits once for the whole call; when it
+  // falls short more steps follow and the reduce runs again.  Earlier batches of a long call
+  // (C4: 92 steps in batches of 16) end without them.
   unsigned long long* h_stats = s->h_stats;
+  bool reduced = false;
+  auto finish = [&]() -> int {  // join the pipelines, reduce, copy the statistics, wait
+    for (int h = 1; h < n_pipes; ++h) {
+      HIP_TRY(hipEventRecord(s->ev_join, pipes[h].st), RT_EDEVICE);
+      HIP_TRY(hipStreamWaitEvent(stream, s->ev_join, 0), RT_EDEVICE);
+    }
+    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    if (stats) HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
+    HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
+    return RT_OK;
+  };
   for (int live = n_pipes; live > 0;) {
     for (int h = 0; h < n_pipes; ++h) {
       Pipe& P = pipes[h];
@@ -2064,16 +2078,15 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
         HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
       }
     }
-    for (int h = 1; h < n_pipes; ++h) {  // the reduce waits for every pipeline's steps
-      if (pipes[h].done) continue;
-      HIP_TRY(hipEventRecord(s->ev_join, pipes[h].st), RT_EDEVICE);
-      HIP_TRY(hipStreamWaitEvent(stream, s->ev_join, 0), RT_EDEVICE);
+    int enq = 0;
+    for (int h = 0; h < n_pipes; ++h) enq = std::max(enq, pipes[h].steps);
+    reduced = enq >= s->last_iters + 1;  // the previous call's steps plus its final (empty) one
+    if (reduced) {
+      if (const int rc = finish()) return rc;
+    } else {
+      for (int h = 0; h < n_pipes; ++h)
+        if (!pipes[h].done) HIP_TRY(hipEventSynchronize(s->ev_b[h][batch - 1]), RT_EDEVICE);
     }
-    hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)((n_pixels + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, la);
-    HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    if (stats) HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
-    HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
-    HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
     for (int h = 0; h < n_pipes; ++h) {
       Pipe& P = pipes[h];
       if (P.done) continue;
@@ -2140,8 +2153,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
         }
       }
     }
-    batch = step_sync ? 1 : 4;  // the previous render's count fell short: top up in small batches
+    // more steps: up to the previous call's count in full batches, past it in small ones
+    batch = step_sync ? 1 : s->last_iters + 1 > enq ? std::max(2, std::min(kMaxHostBatch, s->last_iters + 1 - enq)) : 4;
   }
+  if (!reduced)
+    if (const int rc = finish()) return rc;
   s->last_iters = 0;
   for (int h = 0; h < n_pipes; ++h) s->last_iters = std::max(s->last_iters, pipes[h].iters);
   if (stats) {
