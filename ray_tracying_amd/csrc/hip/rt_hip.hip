@@ -558,16 +558,23 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     t[k] = n0 <= f0 ? n0 : __builtin_inff();
     c[k] = cc[k];
   }
-  // sort 4 (t, entry) ascending
+  // Order the four (t, entry) pairs just enough: three compare-exchanges put the nearest
+  // first (the lane's next item), the pushes below need no order among the other three.  A
+  // full sort (5, RT_SORT_SWAPS A/B build) visits 0.7 % fewer nodes but costs 10 VALU more per
+  // visit: 4727 / 4736 vs 4797 / 4787 Mrays/s on one box (tools/exp_r02_47.sh).
+#ifndef RT_SORT_SWAPS
+#define RT_SORT_SWAPS 3
+#endif
   cswap(t[0], c[0], t[1], c[1]);
   cswap(t[2], c[2], t[3], c[3]);
   cswap(t[0], c[0], t[2], c[2]);
-  cswap(t[1], c[1], t[3], c[3]);
-  cswap(t[1], c[1], t[2], c[2]);
+  if (RT_SORT_SWAPS >= 4) cswap(t[1], c[1], t[3], c[3]);
+  if (RT_SORT_SWAPS >= 5) cswap(t[1], c[1], t[2], c[2]);
   const bool v3 = t[3] != __builtin_inff(), v2 = t[2] != __builtin_inff(), v1 = t[1] != __builtin_inff();
-  // push the three farther children far-to-near.  The entries entered are a prefix of the
-  // sorted four, so unconditional writes at sp, sp+v3, sp+v3+v2 leave exactly those below
-  // the new top (a missed one lands on the top slot and is overwritten or abandoned).
+  // push the three other children (entries 3, 2, 1; far-to-near when fully sorted).  Writes
+  // at sp, sp+v3, sp+v3+v2 -- offsets counting only the children entered -- leave exactly
+  // those below the new top whatever the order (a missed one lands on the next slot and is
+  // overwritten or abandoned).
   if (__ballot(sp + 3 > a.lds_entries) == 0ull) {
     int2* st = S.e + sp * kBlock;
     st[0] = make_int2(c[3], __float_as_int(t[3]));
