@@ -83,10 +83,12 @@ enum Field : int {
                       // nothing for a pinhole camera, whose primary rays start at its location)
   F_COUNT = F_RAY + 7
 };
-// closest-hit record written by the trace kernel, one per slot, AoS (48 B: stored from one
+// closest-hit record written by the trace kernel, one per slot, AoS (32 B: stored from one
 // address by the trace kernel -- no per-field base pointers held in the traversal loop --
-// and read as three float4 by the logic step): point, normal, u, v, material
-enum HitField : int { HIT_P = 0, HIT_N = 3, HIT_U = 6, HIT_V = 7, HIT_MAT = 8, HIT_STRIDE = 12 };
+// and read as two float4 by the logic step): point, normal, material; the (u, v) of
+// textured scenes live in a float2 array of their own (a 48-B record cost every untextured
+// scene 16 B per load)
+enum HitField : int { HIT_P = 0, HIT_N = 3, HIT_MAT = 6, HIT_STRIDE = 8 };
 struct HitRec {
   V3 p, n;
   float u, v;
@@ -94,16 +96,15 @@ struct HitRec {
 };
 __device__ __forceinline__ float* hit_rec(float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
 __device__ __forceinline__ const float* hit_rec(const float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
-// point + normal + material (u, v untouched)
+// point + normal + material
 __device__ __forceinline__ void store_hit_pnm(float* R, V3 p, V3 n, uint32_t mat) {
   *reinterpret_cast<float4*>(R) = make_float4(p.x, p.y, p.z, n.x);
-  *reinterpret_cast<float2*>(R + 4) = make_float2(n.y, n.z);
-  R[HIT_MAT] = __uint_as_float(mat);
+  *reinterpret_cast<float4*>(R + 4) = make_float4(n.y, n.z, __uint_as_float(mat), 0.0f);
 }
+// point + normal + material (u, v: from the uv array, textured scenes only)
 __device__ __forceinline__ HitRec load_hit(const float* R) {
-  const float4 a = *reinterpret_cast<const float4*>(R), b = *reinterpret_cast<const float4*>(R + 4),
-               c = *reinterpret_cast<const float4*>(R + 8);
-  return HitRec{V3{a.x, a.y, a.z}, V3{a.w, b.x, b.y}, b.z, b.w, __float_as_uint(c.x)};
+  const float4 a = *reinterpret_cast<const float4*>(R), b = *reinterpret_cast<const float4*>(R + 4);
+  return HitRec{V3{a.x, a.y, a.z}, V3{a.w, b.x, b.y}, 0.0f, 0.0f, __float_as_uint(b.z)};
 }
 // query record, one per slot: o(3) d(3); TMAX = light distance (shadow) or ray time
 // (closest); KIND bit 0 = shadow any-hit
@@ -176,6 +177,7 @@ struct LogicArgs {
   float* query;          // [Q_COUNT][n_slots]
   int* result;           // [n_slots] (shadow_step_kernel marks consumed results)
   float* hit;            // [n_slots][HIT_STRIDE] (closest hits; written here for transformed shapes)
+  float2* hit_uv;        // [n_slots] (u, v) of closest hits in textured scenes
   int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   int multi_shadow;      // some light has radius > 0 and light_samples > 1: shadow_step_kernel runs first
@@ -213,6 +215,7 @@ struct TraceArgs {
   int n_threads;              // threads of the persistent grid
   unsigned long long* counters;  // box tests, prim tests (count_work)
   float* hit;                 // [n_slots][HIT_STRIDE]: attributes of a closest hit (for the logic step)
+  float2* hit_uv;             // [n_slots]: (u, v) of a closest hit, textured scenes
   int has_tex;                // some material is textured: hit u, v needed
   int refill_min;             // refill kernel: refill finished lanes when fewer than this many traverse
   int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
@@ -404,9 +407,8 @@ __device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const
     HitAttr at;
     float t;
     prim_hit<true, true, true>(P, rec, r, t, &at);
-    float* R = hit_rec(a.hit, slot);
-    store_hit_pnm(R, at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
-    *reinterpret_cast<float2*>(R + HIT_U) = make_float2(at.u, at.v);
+    store_hit_pnm(hit_rec(a.hit, slot), at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
+    a.hit_uv[slot] = make_float2(at.u, at.v);
   }
 }
 
@@ -951,9 +953,8 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
         hu = at.u;
         hv = at.v;
         mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
-        float* R = hit_rec(a.hit, slot);
-        store_hit_pnm(R, hp, hn, (uint32_t)mat_id);
-        if (kTex) *reinterpret_cast<float2*>(R + HIT_U) = make_float2(hu, hv);
+        store_hit_pnm(hit_rec(a.hit, slot), hp, hn, (uint32_t)mat_id);
+        if (kTex) a.hit_uv[slot] = make_float2(hu, hv);
       } else if (st0 == ST_SHADOW || st0 == ST_CLOSEST) {
         // the hit being shaded: its record (written by the trace kernel for planes-only scenes,
         // by the ST_CLOSEST step above otherwise)
@@ -961,8 +962,9 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
         hp = hr.p;
         hn = hr.n;
         if (kTex) {
-          hu = hr.u;
-          hv = hr.v;
+          const float2 uv = a.hit_uv[slot];
+          hu = uv.x;
+          hv = uv.y;
         }
         mat_id = (int)hr.mat;
       }
@@ -1568,6 +1570,7 @@ struct rt_scene_s {
   int* d_result = nullptr;
   float* d_hit = nullptr;
   unsigned int* d_occl = nullptr;  // per slot: occlusion bits of fused shadow rays
+  float2* d_hit_uv = nullptr;      // per slot: (u, v) of the closest hit (textured scenes)
   unsigned int* d_wave_done = nullptr;
   size_t slots_cap = 0;
   unsigned int* h_flag = nullptr;  // pinned: per pipeline, one 128-B line per step of a host batch (any_query copies)
@@ -1585,11 +1588,12 @@ struct rt_scene_s {
 
 static void free_workspace(rt_scene_s* s) {
   void* ptrs[] = {s->d_state, s->d_frames, s->d_refr, s->d_query, s->d_result, s->d_samples, s->d_hit, s->d_wave_done,
-                  s->d_occl};
+                  s->d_occl, s->d_hit_uv};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   s->d_wave_done = nullptr;
   s->d_occl = nullptr;
+  s->d_hit_uv = nullptr;
   s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
   s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr; s->d_hit = nullptr;
   s->slots_cap = 0;
@@ -1831,6 +1835,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_hit, N * HIT_STRIDE * 4), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_hit_uv, N * sizeof(float2)), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_occl, N * 4), RT_ENOMEM);
     HIP_TRY(hipMalloc(&s->d_wave_done, (N / 64 + 1) * 4), RT_ENOMEM);
     if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
@@ -1893,6 +1898,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.query = s->d_query;
   la.result = s->d_result;
   la.hit = s->d_hit;
+  la.hit_uv = s->d_hit_uv;
   la.late_draws = s->late_draws ? 1 : 0;
   la.pinhole = cam->aperture <= 0.0f ? 1 : 0;
   la.multi_shadow = s->soft_lights && p->light_samples > 1 ? 1 : 0;
@@ -1911,6 +1917,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.query = s->d_query;
   ta.result = s->d_result;
   ta.hit = s->d_hit;
+  ta.hit_uv = s->d_hit_uv;
   ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   ta.fetch_shards = fetch_shards_env();
   ta.wave_done = s->d_wave_done;
