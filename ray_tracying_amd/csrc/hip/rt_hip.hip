@@ -1258,8 +1258,9 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
     for (int i = (int)threadIdx.x; i < a.fetch_reset_n; i += kBlock) a.fetch_reset[i * kFetchStride] = 0u;
     if (threadIdx.x == 0) *a.any_query_next = 0u;
   }
-  // only the slot-waves logic_kernel flagged in this step (one scalar load per wave)
-  if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != kWaveIdle) return;
+  // only the slot-waves logic_kernel flagged in this step (one scalar load per wave); every
+  // slot-wave in the call's first step, which also initialises every slot
+  if (!a.first_step && a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != kWaveIdle) return;
   const int N = a.n_slots;
   uint32_t* S = a.state;
   const int lane = (int)(threadIdx.x & 63);
@@ -1281,7 +1282,13 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
   }
   if (lane == 0) a.wave_done[wave] = 0u;
   int px, py, sample;
-  if (!unit_coords(a, unit, px, py, sample)) return;  // edge tile: pixel outside the image (stays idle)
+  if (!unit_coords(a, unit, px, py, sample)) {  // edge tile: pixel outside the image (stays idle)
+    if (a.first_step) {
+      S[F_UNIT * N + slot] = (uint32_t)-2;
+      store_no_query(a.query, N, slot);
+    }
+    return;
+  }
   // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)
   Rng rng;
   rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
@@ -1421,17 +1428,13 @@ __global__ __launch_bounds__(kBlock) void quantise_kernel(const float* rgb, long
   out[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
-// Slot initialisation: every slot idle and every slot-wave flagged for start_kernel, which
-// starts the call's first step (there is nothing for logic_kernel to consume yet).  Block 0
-// also clears the control block and the pipelines' trace counters / any_query lines, and sets
-// each claim counter past the first-step batches (wave w takes batch w = j * shards + w %
-// shards, so shard k's counter starts at the number of waves w with w % shards == k).
+// The call's control state, one block: the control block, the pipelines' trace counters and
+// any_query lines, and each claim counter set past the first step's batches (in the first
+// step slot-wave w takes batch w = j * shards + w % shards without a claim, so shard k's
+// counter starts at the number of waves w with w % shards == k).  The slots themselves are
+// initialised by that first start_kernel, which visits every slot-wave.
 struct InitArgs {
-  uint32_t* state;
   int n_slots;
-  int* result;
-  float* query;
-  unsigned int* wave_done;
   unsigned int* ctl;
   int ctl_words;
   unsigned int* fetch;
@@ -1440,26 +1443,11 @@ struct InitArgs {
   int batch_shards;
 };
 __global__ __launch_bounds__(kBlock) void init_kernel(InitArgs a) {
-  const int slot = blockIdx.x * kBlock + threadIdx.x;
-  if (blockIdx.x == 0) {
-    for (int i = (int)threadIdx.x; i < a.ctl_words; i += kBlock) a.ctl[i] = 0u;
-    for (int i = (int)threadIdx.x; i < a.fetch_words; i += kBlock) a.fetch[i] = 0u;
-    const int waves = a.n_slots >> 6;
-    for (int k = (int)threadIdx.x; k < a.batch_shards; k += kBlock)
-      a.batch_ctr[k * kCtrStride] = (unsigned)(waves / a.batch_shards + (k < waves % a.batch_shards ? 1 : 0));
-  }
-  if (slot >= a.n_slots) return;
-  const int n_slots = a.n_slots;
-  uint32_t* state = a.state;
-  // only the control words: every other field is written by the logic step before it is read
-  // (slots are reused sample after sample without clearing, so nothing may rely on zeros)
-  state[F_UNIT * n_slots + slot] = (uint32_t)-2;  // idle: start_kernel pulls a batch
-  if ((slot & 63) == 0) a.wave_done[slot >> 6] = kWaveIdle;
-  int* result = a.result;
-  float* query = a.query;
-  state[F_CTRL * n_slots + slot] = ST_SAMPLE;
-  result[slot] = -1;
-  store_no_query(query, n_slots, slot);
+  for (int i = (int)threadIdx.x; i < a.ctl_words; i += kBlock) a.ctl[i] = 0u;
+  for (int i = (int)threadIdx.x; i < a.fetch_words; i += kBlock) a.fetch[i] = 0u;
+  const int waves = a.n_slots >> 6;
+  for (int k = (int)threadIdx.x; k < a.batch_shards; k += kBlock)
+    a.batch_ctr[k * kCtrStride] = (unsigned)(waves / a.batch_shards + (k < waves % a.batch_shards ? 1 : 0));
 }
 
 template <bool F, bool T>
@@ -2012,21 +2000,16 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   for (int h = 0; h < n_pipes; ++h) pipes[h].ta.exit_log = exit_log;
 #endif
 
-  const unsigned slot_blocks = (unsigned)((n_slots + kBlock - 1) / kBlock);
   {
     InitArgs ia{};
-    ia.state = s->d_state;
     ia.n_slots = n_slots;
-    ia.result = s->d_result;
-    ia.query = s->d_query;
-    ia.wave_done = s->d_wave_done;
     ia.ctl = ctl;
     ia.ctl_words = kCtlBytes / 4;
     ia.fetch = s->d_fetch;
     ia.fetch_words = (int)(kPipes * kFetchLines * kFetchStride);
     ia.batch_ctr = s->d_batch_ctr;
     ia.batch_shards = la.batch_shards;
-    hipLaunchKernelGGL(init_kernel, dim3(slot_blocks), dim3(kBlock), 0, stream, ia);
+    hipLaunchKernelGGL(init_kernel, dim3(1), dim3(kBlock), 0, stream, ia);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
   }
 
