@@ -887,8 +887,10 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
 #ifndef RT_LOGIC_WAVES_F
 #define RT_LOGIC_WAVES_F 2
 #endif
-template <bool kFrames, bool kTex, bool kPlanes>
-__global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
+// kRefr: the scene has refraction (pending refraction rays in the frames); the reflection-only
+// instance of the frames variant drops that code and fits 4 waves/SIMD (121 VGPRs, 161 with it)
+template <bool kFrames, bool kRefr, bool kTex, bool kPlanes>
+__global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
   const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
   // a wave whose slots all retired has nothing left in this frame (one scalar load)
   if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
@@ -1102,7 +1104,7 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
             }
             refl_ok = dot(rr.d, rr.d) > 0.001f;
           }
-          if (kFrames && m.transparency > 0.0f) {  // createRefractionRay (raytracer.cpp:118-150)
+          if (kRefr && m.transparency > 0.0f) {  // createRefractionRay (raytracer.cpp:118-150)
             V3 N = hn;
             float n_in = 1.0f, n_out = m.refractive_index;
             float cos_i = dot(ray.d, N);
@@ -1184,7 +1186,7 @@ __global__ __launch_bounds__(kBlock, kFrames ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES
                __uint_as_float(F[(FR_A + 2) * N + slot])};
           if (!(meta & 1)) {  // the reflection child returned R
             V3 p{A.x + pm.reflectivity * ret.x, A.y + pm.reflectivity * ret.y, A.z + pm.reflectivity * ret.z};
-            if (meta & 2) {  // refraction pending: trace it as the next child
+            if (kRefr && (meta & 2)) {  // refraction pending: trace it as the next child
               uint32_t* Fw = a.frames + (size_t)depth * FR_COUNT * N;
               Fw[(FR_A + 0) * N + slot] = __float_as_uint(p.x);
               Fw[(FR_A + 1) * N + slot] = __float_as_uint(p.y);
@@ -1450,10 +1452,10 @@ __global__ __launch_bounds__(kBlock) void init_kernel(InitArgs a) {
     a.batch_ctr[k * kCtrStride] = (unsigned)(waves / a.batch_shards + (k < waves % a.batch_shards ? 1 : 0));
 }
 
-template <bool F, bool T>
+template <bool F, bool R, bool T>
 void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_t st) {
-  if (planes) hipLaunchKernelGGL((logic_kernel<F, T, true>), dim3(blocks), dim3(kBlock), 0, st, la);
-  else hipLaunchKernelGGL((logic_kernel<F, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
+  if (planes) hipLaunchKernelGGL((logic_kernel<F, R, T, true>), dim3(blocks), dim3(kBlock), 0, st, la);
+  else hipLaunchKernelGGL((logic_kernel<F, R, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
 }
 // trace launch (the refill kernel; count: the instrumented variant)
 void launch_trace(const TraceArgs& ta, bool count, bool planes, unsigned blocks, size_t lds, hipStream_t st) {
@@ -1497,13 +1499,16 @@ static int refill_min_env() {
   return v;
 }
 
-void launch_logic(const LogicArgs& la, bool frames, bool tex, bool planes, unsigned blocks, hipStream_t st) {
-  if (frames) {
-    if (tex) launch_logic2<true, true>(la, planes, blocks, st);
-    else launch_logic2<true, false>(la, planes, blocks, st);
+void launch_logic(const LogicArgs& la, bool frames, bool refr, bool tex, bool planes, unsigned blocks, hipStream_t st) {
+  if (frames && refr) {
+    if (tex) launch_logic2<true, true, true>(la, planes, blocks, st);
+    else launch_logic2<true, true, false>(la, planes, blocks, st);
+  } else if (frames) {
+    if (tex) launch_logic2<true, false, true>(la, planes, blocks, st);
+    else launch_logic2<true, false, false>(la, planes, blocks, st);
   } else {
-    if (tex) launch_logic2<false, true>(la, planes, blocks, st);
-    else launch_logic2<false, false>(la, planes, blocks, st);
+    if (tex) launch_logic2<false, false, true>(la, planes, blocks, st);
+    else launch_logic2<false, false, false>(la, planes, blocks, st);
   }
 }
 
@@ -1690,6 +1695,12 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   rt_scene_s* s = new rt_scene_s();
   s->device = device;
   s->desc = *d;
+  // the kernel variants follow these flags (recursion frames, refraction): derived from the
+  // materials here as well, so a caller's desc cannot select a variant that drops a path
+  for (int i = 0; i < d->n_materials; ++i) {
+    if (d->materials[i].reflectivity > 0.0f) s->desc.flags |= RT_SCENE_HAS_REFLECTION;
+    if (d->materials[i].transparency > 0.0f) s->desc.flags |= RT_SCENE_HAS_REFRACTION;
+  }
   for (int i = 0; i < d->n_lights; ++i) s->soft_lights = s->soft_lights || d->lights[i].radius > 0.0f;
   // fused shadow rays: planes-only scenes whose lights are all points (one shadow ray each,
   // no random draws), at most 24 of them (occlusion bits of one word)
@@ -2064,7 +2075,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
             hipLaunchKernelGGL(shadow_step_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
             HIP_TRY(hipGetLastError(), RT_EDEVICE);
           }
-          launch_logic(P.la, need_frames, tex, planes_only, P.logic_blocks, P.st);
+          launch_logic(P.la, need_frames, need_refr, tex, planes_only, P.logic_blocks, P.st);
           HIP_TRY(hipGetLastError(), RT_EDEVICE);
         }
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
