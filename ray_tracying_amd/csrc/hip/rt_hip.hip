@@ -225,6 +225,10 @@ struct TraceArgs {
   const rt_light* lights;
   int n_fuse;
   unsigned int* occl;
+  // kSoft launches: a finished soft-light shadow sample with samples left draws and traces
+  // the next one in the same lane (shadow_step_kernel's ops on the slot's state)
+  uint32_t* state;
+  int light_samples;
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
@@ -626,7 +630,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 4  // waves per SIMD the register allocation targets (A/B builds: make variant)
 #endif
-template <bool kCount, bool kPlanesOnly, bool kFuse>
+template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_work;
@@ -681,9 +685,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
   };
   // the lane's query is complete: write it back and free the lane (kFuse: a closest hit goes
   // on to its lights' shadow rays first; their occlusion bits are written after the last)
+  // kSoft: the slot's light (a sphere light) still has samples to draw after this one: add
+  // this sample's visibility, draw the next target and start its traversal (shade's loop,
+  // raytracer.cpp:214-236, as shadow_step_kernel does it); false when the light is done
+  auto soft_next = [&](bool occluded) -> bool {
+    const int N = a.n_slots;
+    uint32_t* S = a.state;
+    const uint32_t lw = S[F_LIGHT * N + slot];
+    const int light = (int)(lw & 0xffffu), ls = (int)(lw >> 16);
+    const rt_light& L = a.lights[light];
+    if (!(L.radius > 0.0f && ls + 1 < a.light_samples)) return false;
+    float vis = ls > 0 ? __uint_as_float(S[F_VIS * N + slot]) : 0.0f;
+    if (!occluded) vis += 1.0f;
+    Rng rng;
+    rng.key = (uint64_t)S[F_KEY * N + slot] | ((uint64_t)S[(F_KEY + 1) * N + slot] << 32);
+    rng.ctr = S[F_RNG * N + slot];
+    const HitRec hr = load_hit(hit_rec(a.hit, slot));
+    V3 target{L.location[0], L.location[1], L.location[2]};
+    target = add(target, mul(rng.in_unit_sphere(), L.radius));
+    const V3 lv = sub(target, hr.p);
+    const float tmax = sqrtf(dot(lv, lv));
+    S[F_LIGHT * N + slot] = (uint32_t)light | ((uint32_t)(ls + 1) << 16);
+    S[F_VIS * N + slot] = __float_as_uint(vis);
+    S[F_RNG * N + slot] = rng.ctr;
+    setup_query(q, add(hr.p, mul(hr.n, 1e-4f)), normalize(lv), tmax, true);
+    ++nrays;
+    if (kCount) ++dg_any_rays;
+    start_traversal();
+    return true;
+  };
   auto settle = [&]() {
     int next = -1;  // kFuse: the light whose shadow ray the lane traces next
-    if (kFuse && fz != 0) {
+    if (kSoft && q.any) {
+      complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+      if (soft_next(h.done)) return;
+      a.result[slot] = h.done ? 1 : 0;
+    } else if (kFuse && fz != 0) {
       complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
       const int l = (fz & 0xff) - 1;
       const unsigned bits = ((unsigned)fz >> 8) | (h.done ? 1u << l : 0u);
@@ -1458,17 +1495,23 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
   else hipLaunchKernelGGL((logic_kernel<F, R, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
 }
 // trace launch (the refill kernel; count: the instrumented variant)
-void launch_trace(const TraceArgs& ta, bool count, bool planes, unsigned blocks, size_t lds, hipStream_t st) {
-  const bool fuse = ta.n_fuse > 0;  // planes-only scenes only (the host's choice)
-  if (count) {
-    if (fuse) hipLaunchKernelGGL((trace_refill_kernel<true, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    else if (planes) hipLaunchKernelGGL((trace_refill_kernel<true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    else hipLaunchKernelGGL((trace_refill_kernel<true, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-  } else {
-    if (fuse) hipLaunchKernelGGL((trace_refill_kernel<false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    else if (planes) hipLaunchKernelGGL((trace_refill_kernel<false, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-    else hipLaunchKernelGGL((trace_refill_kernel<false, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-  }
+template <bool kCount>
+void launch_trace2(const TraceArgs& ta, bool planes, bool soft, unsigned blocks, size_t lds, hipStream_t st) {
+  if (ta.n_fuse > 0)  // planes-only scenes with point lights only (the host's choice)
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else if (soft && planes)
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else if (soft)
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else if (planes)
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+}
+// trace launch: soft = the lanes continue soft-light shadow samples themselves (kSoft)
+void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, unsigned blocks, size_t lds, hipStream_t st) {
+  if (count) launch_trace2<true>(ta, planes, soft, blocks, lds, st);
+  else launch_trace2<false>(ta, planes, soft, blocks, lds, st);
 }
 static int fetch_shards_env() {
   static const int v = [] {
@@ -1741,7 +1784,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const int lds_entries = std::min(d->stack_bound, lds_stack_entries());
     const bool planes = d->prim_stride == 64;
-    const void* fn = planes ? (const void*)trace_refill_kernel<false, true, false> : (const void*)trace_refill_kernel<false, false, false>;
+    const void* fn = planes ? (const void*)trace_refill_kernel<false, true, false, false> : (const void*)trace_refill_kernel<false, false, false, false>;
     const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kBlock, lds_bytes) != hipSuccess || bpc < 1)
       bpc = 2;
@@ -1900,7 +1943,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.hit_uv = s->d_hit_uv;
   la.late_draws = s->late_draws ? 1 : 0;
   la.pinhole = cam->aperture <= 0.0f ? 1 : 0;
-  la.multi_shadow = s->soft_lights && p->light_samples > 1 ? 1 : 0;
+  // Soft-light shadow samples after a light's first: drawn and traced by the lane that traced
+  // the previous one (kSoft trace launches, default), or advanced by shadow_step_kernel
+  // (RT_SOFT_FUSE=0), or by the logic kernel itself (RT_SOFT_FUSE=0 RT_SHADOW_STEP=0)
+  const bool soft_scene = s->soft_lights && p->light_samples > 1;
+  bool soft_trace = soft_scene;
+  if (const char* e = std::getenv("RT_SOFT_FUSE")) soft_trace = soft_trace && std::atoi(e) != 0;
+  la.multi_shadow = soft_scene && !soft_trace ? 1 : 0;
   if (const char* e = std::getenv("RT_SHADOW_STEP")) la.multi_shadow = la.multi_shadow && std::atoi(e) != 0;
   la.wave_done = s->d_wave_done;
   la.batch_ctr = s->d_batch_ctr;
@@ -1928,6 +1977,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.leaf_min = leaf_min_env();
   ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
   ta.lights = (const rt_light*)s->d_lights;
+  ta.state = s->d_state;
+  ta.light_samples = p->light_samples;
   // Fused shadow rays pay when the call is small (at most two slot loads of samples: one
   // rank's share of a split frame): each launch ends in a drain of ~0.45 ms that is the same
   // for any launch size, and fusing halves the launches.  On a whole frame the lanes' camera
@@ -1945,6 +1996,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   int replay_iter = -1, replay_reps = 0;
   const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
   if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
+  if (soft_trace) replay_iter = -1;  // a replay would draw the soft-light samples again from advanced state
   // the diagnostics wait on every step (one pipeline)
 #ifdef RT_EXIT_TIMING
   const bool step_sync = true;
@@ -2081,7 +2133,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
-        launch_trace(P.ta, p->count_work != 0, planes_only, P.trace_blocks, lds, P.st);
+        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, P.trace_blocks, lds, P.st);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
       }
@@ -2111,7 +2163,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
           for (int r = 0; r < replay_reps; ++r) {
             HIP_TRY(hipMemsetAsync(P.ta.fetch, 0, (size_t)ta.fetch_shards * kFetchStride * 4, stream), RT_EDEVICE);
             HIP_TRY(hipEventRecord(s->ev_a[0][1], stream), RT_EDEVICE);
-            launch_trace(P.ta, false, planes_only, P.trace_blocks, lds, stream);
+            launch_trace(P.ta, false, planes_only, soft_trace, P.trace_blocks, lds, stream);
             HIP_TRY(hipEventRecord(s->ev_b[0][1], stream), RT_EDEVICE);
             HIP_TRY(hipEventSynchronize(s->ev_b[0][1]), RT_EDEVICE);
             float m = 0.f;

@@ -4,9 +4,10 @@ Each knob is read once per process (environment), so every configuration renders
 child process and must match the oracle bit for bit: the LDS traversal stack cut to 2
 entries (every deeper entry spills to HBM), extreme refill / leaf-phase thresholds, one and
 many work-counter shards, a slot count so small that a frame takes dozens of steps, and the
-slots split into two pipelines on two streams, and soft-shadow samples advanced by the logic
-kernel instead of shadow_step_kernel, and the greedy BVH4 collapse instead of the
-SAH-optimal one, and point-light shadow rays left unfused in a small call.
+slots split into two pipelines on two streams, soft-shadow samples advanced by
+shadow_step_kernel or by the logic kernel instead of the tracing lane, the greedy BVH4
+collapse instead of the SAH-optimal one, and point-light shadow rays left unfused in a small
+call.
 """
 import os
 import subprocess
@@ -42,7 +43,8 @@ KNOBS = [
     {"RT_MAX_UNITS": "3000"},  # the call runs as many tile chunks
     {"RT_PIPES": "2"},  # two slot pipelines on two streams
     {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
-    {"RT_SHADOW_STEP": "0"},  # soft-shadow samples advanced by the logic kernel itself
+    {"RT_SOFT_FUSE": "0"},  # soft-shadow samples advanced by shadow_step_kernel, not the tracing lane
+    {"RT_SOFT_FUSE": "0", "RT_SHADOW_STEP": "0"},  # ... or by the logic kernel itself
     {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
     {"RT_FUSE": "0"},  # point-light shadow rays as their own queries (small calls fuse them by default)
 ]
