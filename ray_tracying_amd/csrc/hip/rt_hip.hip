@@ -52,7 +52,10 @@ static int lds_stack_entries() {  // read per call: tests vary it within one pro
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
 constexpr int kCtlBytes = 4096;    // control block (cleared by init_kernel)
-constexpr int kStatsBytes = 512;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
+constexpr int kStatsBytes = 512;
+// scenes with fewer primitives spend their frame in the per-step passes over the slots, not in
+// traversal: their shadow rays are fused whatever the call size
+constexpr int kFuseFewPrims = 65536;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
 // Batch-claim counters of the logic step: one per 128-B line (kCtrStride words apart) --
 // atomics on one line serialise at the memory side, so the shards must not share lines.
 constexpr int kMaxBatchShards = 1024;
@@ -734,6 +737,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
     } else {
       finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
       if (kFuse && !q.any && h.best_idx >= 0) {
+        if (!kPlanesOnly) {  // transformed shapes: the hit record the logic step would compute
+          const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
+          PrimA P;
+          load_prim_a(rec, P);
+          HitAttr at;
+          float t;
+          prim_hit<true, false, false>(P, rec, q.r, t, &at);
+          store_hit_pnm(hit_rec(a.hit, slot), at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
+        }
         fz = 1;
         next = 0;
       }
@@ -975,7 +987,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
       const V3 cam_o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
       if (fast) {
         want = true;
-      } else if (!kPlanes && st0 == ST_CLOSEST && res_ld >= 0) {
+      } else if (!kPlanes && st0 == ST_CLOSEST && res_ld >= 0 && a.n_fuse == 0) {
         // the hit being shaded (raytracer.cpp:293-303): the hit primitive's test with
         // attributes on the ray just traced (the query record), kept in the slot's hit record
         // for the shadow steps that follow
@@ -1497,8 +1509,10 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
 // trace launch (the refill kernel; count: the instrumented variant)
 template <bool kCount>
 void launch_trace2(const TraceArgs& ta, bool planes, bool soft, unsigned blocks, size_t lds, hipStream_t st) {
-  if (ta.n_fuse > 0)  // planes-only scenes with point lights only (the host's choice)
+  if (ta.n_fuse > 0 && planes)  // point lights only (the host's choice)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else if (ta.n_fuse > 0)  // ... and no textures: the fused path stores no (u, v)
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (soft && planes)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (soft)
@@ -1743,11 +1757,14 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   for (int i = 0; i < d->n_materials; ++i) {
     if (d->materials[i].reflectivity > 0.0f) s->desc.flags |= RT_SCENE_HAS_REFLECTION;
     if (d->materials[i].transparency > 0.0f) s->desc.flags |= RT_SCENE_HAS_REFRACTION;
+    if (d->materials[i].texture >= 0) s->desc.flags |= RT_SCENE_HAS_TEXTURE;
   }
   for (int i = 0; i < d->n_lights; ++i) s->soft_lights = s->soft_lights || d->lights[i].radius > 0.0f;
-  // fused shadow rays: planes-only scenes whose lights are all points (one shadow ray each,
-  // no random draws), at most 24 of them (occlusion bits of one word)
-  s->fuse_lights = d->prim_stride == 64 && !s->soft_lights && d->n_lights >= 1 && d->n_lights <= 24 ? d->n_lights : 0;
+  // fused shadow rays: scenes whose lights are all points (one shadow ray each, no random
+  // draws), at most 24 of them (occlusion bits of one word); with transformed shapes only
+  // untextured ones (the tracing lane computes the hit's point and normal, not its (u, v))
+  s->fuse_lights = (d->prim_stride == 64 || !(s->desc.flags & RT_SCENE_HAS_TEXTURE)) && !s->soft_lights &&
+                   d->n_lights >= 1 && d->n_lights <= 24 ? d->n_lights : 0;
   s->late_draws = s->soft_lights;
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
   int rc = RT_OK;
@@ -1979,12 +1996,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
   ta.light_samples = p->light_samples;
-  // Fused shadow rays pay when the call is small (at most two slot loads of samples: one
-  // rank's share of a split frame): each launch ends in a drain of ~0.45 ms that is the same
-  // for any launch size, and fusing halves the launches.  On a whole frame the lanes' camera
-  // and shadow rays then interleave within a wave and lose coherence (headline -6.5 %).
+  // Fused shadow rays halve the steps of a sample.  They pay when the call is small (at most
+  // two slot loads of samples: one rank's share of a split frame; each launch ends in a drain
+  // of ~0.45 ms whatever its size) and when the scene has few primitives (its frame is spent
+  // in the per-step passes over the slots); on a whole frame of a large scene the lanes'
+  // camera and shadow rays interleave within a wave and lose coherence (headline -6.5 %).
   // RT_FUSE=0 / 1 overrides (1: whenever the scene allows it).
-  ta.n_fuse = n_units <= 2LL * n_slots ? s->fuse_lights : 0;
+  ta.n_fuse = n_units <= 2LL * n_slots || s->desc.n_prims < kFuseFewPrims ? s->fuse_lights : 0;
   if (const char* e = std::getenv("RT_FUSE")) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;

@@ -1,6 +1,6 @@
-"""Fused shadow rays (trace_refill_kernel<.., kFuse>): in a planes-only scene lit by point
-lights only, the lane that finds a closest hit traces its lights' shadow rays right after it
-and leaves occlusion bits for the logic step.  Fused and unfused renders must both match the
+"""Fused shadow rays (trace_refill_kernel<.., kFuse>): in a scene lit by point lights only
+(planes, or untextured transformed shapes), the lane that finds a closest hit traces its
+lights' shadow rays right after it and leaves occlusion bits for the logic step.  Fused and unfused renders must both match the
 oracle bit for bit (and in ray count): with reflection, refraction and glossy fuzz after the
 shade (raytracer.cpp:180-350), in BVH and linear modes, and with 24 lights (the last bit of the
 occlusion word).  RT_FUSE is read per call, so each setting renders in a child process like
@@ -40,6 +40,31 @@ def render_child(path, out, spp, bvh, fuse):
 @pytest.mark.parametrize("bvh", [True, False])
 def test_fused_shadows_match_oracle(tmp_path, gpu, bvh):
     p = scenes.write(scenes.planes_lit(), str(tmp_path / "p.json"))
+    ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=9, spp_sqrt=2, light_samples=1, use_bvh=bvh)
+    for fuse in ("1", "0"):
+        img, rays = render_child(p, str(tmp_path / f"img{fuse}.npy"), 2, bvh, fuse)
+        diff = int((img.view(np.uint32) != ref.view(np.uint32)).sum())
+        assert diff == 0, f"RT_FUSE={fuse}: {diff} channels differ"
+        assert rays == ost["rays"], fuse
+
+
+def point_lit_features():
+    """features() (spheres incl. a moving one, cubes, rectangles, planes; mirror, glass, glossy)
+    with point lights and no textures: the fused path for transformed shapes, whose hit
+    record the tracing lane computes (prim_hit with attributes) before the shadow rays."""
+    sc = scenes.features(res=(40, 32))
+    for light in sc["lights"]:
+        light["radius"] = 0.0
+    for k in ("spheres", "cubes", "rectangles", "planes"):
+        for o in sc.get(k, []):
+            if isinstance(o.get("material"), dict):
+                o["material"].pop("texture_file", None)
+    return sc
+
+
+@pytest.mark.parametrize("bvh", [True, False])
+def test_fused_shadows_transformed_shapes(tmp_path, gpu, bvh):
+    p = scenes.write(point_lit_features(), str(tmp_path / "f.json"))
     ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=9, spp_sqrt=2, light_samples=1, use_bvh=bvh)
     for fuse in ("1", "0"):
         img, rays = render_child(p, str(tmp_path / f"img{fuse}.npy"), 2, bvh, fuse)
