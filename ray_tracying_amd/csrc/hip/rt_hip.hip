@@ -232,6 +232,11 @@ struct TraceArgs {
   // the next one in the same lane (shadow_step_kernel's ops on the slot's state)
   uint32_t* state;
   int light_samples;
+  // kSoft launches with soft_start: a closest hit also starts its shade loop -- the first
+  // shadow sample of light 0, as the logic step would emit it (then continued as above);
+  // frames / pinhole tell which of the closest ray's words the shading step reads back
+  int soft_start;
+  int frames, pinhole;
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
@@ -717,6 +722,44 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
     start_traversal();
     return true;
   };
+  // kSoft + soft_start: shade's first shadow ray for the closest hit just found (the logic
+  // step's transition ST_CLOSEST -> ST_SHADOW, raytracer.cpp:180-236: light 0, sample 0)
+  auto soft_first = [&]() {
+    const int N = a.n_slots;
+    uint32_t* S = a.state;
+    const uint32_t depth = S[F_CTRL * N + slot] >> 4;
+    const HitRec hr = load_hit(hit_rec(a.hit, slot));
+    const rt_light& L = a.lights[0];
+    V3 target{L.location[0], L.location[1], L.location[2]};
+    if (L.radius > 0.0f) {
+      Rng rng;
+      rng.key = (uint64_t)S[F_KEY * N + slot] | ((uint64_t)S[(F_KEY + 1) * N + slot] << 32);
+      rng.ctr = S[F_RNG * N + slot];
+      target = add(target, mul(rng.in_unit_sphere(), L.radius));
+      S[F_RNG * N + slot] = rng.ctr;
+    }
+    const V3 lv = sub(target, hr.p);
+    const float tmax = sqrtf(dot(lv, lv));
+    S[F_CTRL * N + slot] = (uint32_t)ST_SHADOW | (depth << 4);
+    S[F_LIGHT * N + slot] = 0u;
+    if (a.frames) {  // the traced ray, read back by the shading (view vector) and reflection
+      S[(F_RAY + 0) * N + slot] = __float_as_uint(q.r.o.x);
+      S[(F_RAY + 1) * N + slot] = __float_as_uint(q.r.o.y);
+      S[(F_RAY + 2) * N + slot] = __float_as_uint(q.r.o.z);
+      S[(F_RAY + 3) * N + slot] = __float_as_uint(q.r.d.x);
+      S[(F_RAY + 4) * N + slot] = __float_as_uint(q.r.d.y);
+      S[(F_RAY + 5) * N + slot] = __float_as_uint(q.r.d.z);
+      S[(F_RAY + 6) * N + slot] = __float_as_uint(q.r.time);
+    } else if (!a.pinhole) {
+      S[(F_RAY + 0) * N + slot] = __float_as_uint(q.r.o.x);
+      S[(F_RAY + 1) * N + slot] = __float_as_uint(q.r.o.y);
+      S[(F_RAY + 2) * N + slot] = __float_as_uint(q.r.o.z);
+    }
+    setup_query(q, add(hr.p, mul(hr.n, 1e-4f)), normalize(lv), tmax, true);
+    ++nrays;
+    if (kCount) ++dg_any_rays;
+    start_traversal();
+  };
   auto settle = [&]() {
     int next = -1;  // kFuse: the light whose shadow ray the lane traces next
     if (kSoft && q.any) {
@@ -736,7 +779,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
       }
     } else {
       finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
-      if (kFuse && !q.any && h.best_idx >= 0) {
+      if ((kFuse || (kSoft && a.soft_start)) && !q.any && h.best_idx >= 0) {
         if (!kPlanesOnly) {  // transformed shapes: the hit record the logic step would compute
           const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
           PrimA P;
@@ -745,6 +788,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
           float t;
           prim_hit<true, false, false>(P, rec, q.r, t, &at);
           store_hit_pnm(hit_rec(a.hit, slot), at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
+        }
+        if (kSoft) {
+          soft_first();
+          return;
         }
         fz = 1;
         next = 0;
@@ -1996,6 +2043,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
   ta.light_samples = p->light_samples;
+  // the closest hit starts its shade loop in the tracing lane too: planes, or untextured
+  // transformed shapes (that lane computes point and normal, not (u, v)); RT_SOFT_START=0 off
+  ta.soft_start = soft_trace && s->desc.n_lights >= 1 && (planes_only || !(s->desc.flags & RT_SCENE_HAS_TEXTURE)) ? 1 : 0;
+  if (const char* e = std::getenv("RT_SOFT_START")) ta.soft_start = ta.soft_start && std::atoi(e) != 0;
+  ta.frames = need_frames ? 1 : 0;
+  ta.pinhole = cam->aperture <= 0.0f ? 1 : 0;
   // Fused shadow rays halve the steps of a sample.  They pay when the call is small (at most
   // two slot loads of samples: one rank's share of a split frame; each launch ends in a drain
   // of ~0.45 ms whatever its size) and when the scene has few primitives (its frame is spent

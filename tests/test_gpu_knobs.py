@@ -43,6 +43,7 @@ KNOBS = [
     {"RT_MAX_UNITS": "3000"},  # the call runs as many tile chunks
     {"RT_PIPES": "2"},  # two slot pipelines on two streams
     {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
+    {"RT_SOFT_START": "0"},  # a closest hit's first shadow sample emitted by the logic step
     {"RT_SOFT_FUSE": "0"},  # soft-shadow samples advanced by shadow_step_kernel, not the tracing lane
     {"RT_SOFT_FUSE": "0", "RT_SHADOW_STEP": "0"},  # ... or by the logic kernel itself
     {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
