@@ -23,16 +23,18 @@ import sys
 import numpy as np
 sys.path.insert(0, sys.argv[1])
 import ray_tracying_amd as rt
-sc = rt.Scene(sys.argv[2])
-img, st = sc.render(rt.RenderParams(spp_sqrt=int(sys.argv[4]), light_samples=1, use_bvh=sys.argv[5] == "1", seed=9))
+sc = rt.Scene(sys.argv[2], texture_root=sys.argv[7])
+img, st = sc.render(rt.RenderParams(spp_sqrt=int(sys.argv[4]), light_samples=int(sys.argv[6]), use_bvh=sys.argv[5] == "1",
+                                    seed=9))
 np.save(sys.argv[3], img)
 print(st.rays)
 """
 
 
-def render_child(path, out, spp, bvh, fuse):
-    r = subprocess.run([sys.executable, "-c", CHILD, ROOT, path, out, str(spp), "1" if bvh else "0"],
-                       env={**os.environ, "RT_FUSE": fuse}, capture_output=True, text=True, timeout=120)
+def render_child(path, out, spp, bvh, fuse, light_samples=1, env=None):
+    r = subprocess.run([sys.executable, "-c", CHILD, ROOT, path, out, str(spp), "1" if bvh else "0", str(light_samples),
+                        scenes.TEXTURES], env={**os.environ, "RT_FUSE": fuse, **(env or {})}, capture_output=True,
+                       text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     return np.load(out), int(r.stdout.strip().splitlines()[-1])
 
@@ -77,5 +79,34 @@ def test_fused_24_lights(tmp_path, gpu):
     p = scenes.write(scenes.planes_lit(n=150, res=(24, 16), n_lights=24), str(tmp_path / "p24.json"))
     ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=9, spp_sqrt=1, light_samples=1, use_bvh=True)
     img, rays = render_child(p, str(tmp_path / "img.npy"), 1, True, "1")
+    assert int((img.view(np.uint32) != ref.view(np.uint32)).sum()) == 0
+    assert rays == ost["rays"]
+
+
+def test_fused_textured_planes(tmp_path, gpu):
+    """Fused shadows on textured planes: the closest hit's (u, v) go to the uv array."""
+    sc = scenes.planes_lit()
+    for k, pl in enumerate(sc["planes"]):
+        if k % 3 == 0:
+            pl["material"]["texture_file"] = "checker.jpg"
+    p = scenes.write(sc, str(tmp_path / "t.json"))
+    ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=9, spp_sqrt=2, light_samples=1, use_bvh=True,
+                            texture_root=scenes.TEXTURES)
+    for fuse in ("1", "0"):
+        img, rays = render_child(p, str(tmp_path / f"img{fuse}.npy"), 2, True, fuse)
+        assert int((img.view(np.uint32) != ref.view(np.uint32)).sum()) == 0, fuse
+        assert rays == ost["rays"], fuse
+
+
+@pytest.mark.parametrize("start", ["1", "0"])
+def test_soft_samples_in_lane_planes(tmp_path, gpu, start):
+    """Soft-light samples drawn and traced by the tracing lane on a planes-only scene (kSoft),
+    the first one started by the closest hit itself or by the logic step (RT_SOFT_START)."""
+    sc = scenes.planes_lit(n_lights=2)
+    sc["lights"][0]["radius"] = 0.4
+    p = scenes.write(sc, str(tmp_path / "s.json"))
+    ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=9, spp_sqrt=2, light_samples=3, use_bvh=True)
+    img, rays = render_child(p, str(tmp_path / "img.npy"), 2, True, "1", light_samples=3,
+                             env={"RT_SOFT_START": start})
     assert int((img.view(np.uint32) != ref.view(np.uint32)).sum()) == 0
     assert rays == ost["rays"]
