@@ -143,7 +143,9 @@ typedef struct rt_scene_desc {
   int64_t n_texel_bytes;
   const uint8_t* texels;
   float scene_scale; /* max |coordinate| of scene bounds and camera, for pruning margins */
-  int32_t flags;     /* RT_SCENE_* feature bits */
+  int32_t flags;     /* RT_SCENE_* feature bits; rt_scene_create also derives them from the
+                        materials (reflectivity, transparency > 0, texture >= 0), so a desc
+                        that omits one cannot select a kernel variant that drops its path */
 } rt_scene_desc;
 
 #define RT_SCENE_HAS_REFLECTION 1
