@@ -183,7 +183,7 @@ struct LogicArgs {
   float2* hit_uv;        // [n_slots] (u, v) of closest hits in textured scenes
   int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
-  int multi_shadow;      // some light has radius > 0 and light_samples > 1: shadow_step_kernel runs first
+  int multi_shadow;      // soft lights, light_samples > 1, RT_SOFT_FUSE=0: shadow_step_kernel runs first
   unsigned int* any_query;  // set to 1 by every wave that emits a query (plain store)
   // per-step resets done by start_kernel's first block (no fill launches between kernels):
   // the trace work counters of this step and the other any_query line (the next step's flag;
@@ -1348,8 +1348,9 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
 // samples: coherent rays -- from its counter shard (one 128-B line per shard), and each
 // slot starts its sample: compute_pixel_color's jittered sub-position and the camera ray
 // (raytracer.cpp:18-70, camera.cpp:98-179), whose closest-hit query it emits.  Runs after
-// logic_kernel in every step (the same step in which a wave's last sample finishes), at
-// 8 waves per SIMD: the sample-start code kept in logic_kernel cost it 36 registers.
+// logic_kernel in every step (the same step in which a wave's last sample finishes) and
+// alone in the call's first step, where it visits every slot-wave and initialises every
+// slot; 8 waves per SIMD: the sample-start code kept in logic_kernel cost it 36 registers.
 __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
   const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
   if (blockIdx.x == 0) {  // this step's trace counters, and the next step's any_query line
