@@ -119,16 +119,26 @@ struct QueryRec {
   float tq;
   int kind;
 };
-__device__ __forceinline__ QueryRec load_query(const float* Q, int N, int slot) {
-  return QueryRec{V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]},
-                  V3{Q[(Q_D + 0) * N + slot], Q[(Q_D + 1) * N + slot], Q[(Q_D + 2) * N + slot]},
-                  Q[Q_TMAX * N + slot], __float_as_int(Q[Q_KIND * N + slot])};
+// KIND bit 1: a pinhole camera's primary ray, whose origin (the camera location) is not
+// stored -- 12 B less per camera ray for start_kernel to write and the traversal to read
+constexpr int kQueryCamOrigin = 2;
+__device__ __forceinline__ QueryRec load_query(const float* Q, int N, int slot, const float* cam_loc) {
+  const int kind = __float_as_int(Q[Q_KIND * N + slot]);
+  const V3 o = (kind & kQueryCamOrigin) ? V3{cam_loc[0], cam_loc[1], cam_loc[2]}
+                                        : V3{Q[(Q_O + 0) * N + slot], Q[(Q_O + 1) * N + slot], Q[(Q_O + 2) * N + slot]};
+  return QueryRec{o, V3{Q[(Q_D + 0) * N + slot], Q[(Q_D + 1) * N + slot], Q[(Q_D + 2) * N + slot]}, Q[Q_TMAX * N + slot],
+                  kind};
 }
 __device__ __forceinline__ void store_query(float* Q, int N, int slot, V3 o, V3 d, float tq, int kind) {
   Q[(Q_O + 0) * N + slot] = o.x; Q[(Q_O + 1) * N + slot] = o.y; Q[(Q_O + 2) * N + slot] = o.z;
   Q[(Q_D + 0) * N + slot] = d.x; Q[(Q_D + 1) * N + slot] = d.y; Q[(Q_D + 2) * N + slot] = d.z;
   Q[Q_TMAX * N + slot] = tq;
   Q[Q_KIND * N + slot] = __int_as_float(kind);
+}
+__device__ __forceinline__ void store_cam_query(float* Q, int N, int slot, V3 d, float tq) {
+  Q[(Q_D + 0) * N + slot] = d.x; Q[(Q_D + 1) * N + slot] = d.y; Q[(Q_D + 2) * N + slot] = d.z;
+  Q[Q_TMAX * N + slot] = tq;
+  Q[Q_KIND * N + slot] = __int_as_float(kQueryCamOrigin);
 }
 __device__ __forceinline__ void store_no_query(float* Q, int N, int slot) { Q[Q_KIND * N + slot] = __int_as_float(-1); }
 // frames for depths 0..kMaxDepth-1: A(3) + meta, and the pending refraction ray (6)
@@ -209,6 +219,7 @@ struct TraceArgs {
   unsigned int* fetch;        // fetch_shards work counters over slot slices (zeroed per step)
   int fetch_shards;
   const unsigned int* any_query;  // logic's "some slot has a query" flag for this step
+  float cam_loc[3];           // origin of the queries marked kQueryCamOrigin
   unsigned int* host_flag;    // pinned host word: any_query of this step, for the host's loop
   unsigned long long* rays;   // queries traced (one atomic per wave at exit)
   int n_slots;                // field stride of the per-slot arrays
@@ -383,8 +394,10 @@ __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query&
   const int N = a.n_slots;
   const int kind = __float_as_int(a.query[Q_KIND * N + slot]);
   if (kind < 0) return false;
-  setup_query(q, V3{a.query[(Q_O + 0) * N + slot], a.query[(Q_O + 1) * N + slot], a.query[(Q_O + 2) * N + slot]},
-              V3{a.query[(Q_D + 0) * N + slot], a.query[(Q_D + 1) * N + slot], a.query[(Q_D + 2) * N + slot]},
+  const V3 o = (kind & kQueryCamOrigin)
+                   ? V3{a.cam_loc[0], a.cam_loc[1], a.cam_loc[2]}
+                   : V3{a.query[(Q_O + 0) * N + slot], a.query[(Q_O + 1) * N + slot], a.query[(Q_O + 2) * N + slot]};
+  setup_query(q, o, V3{a.query[(Q_D + 0) * N + slot], a.query[(Q_D + 1) * N + slot], a.query[(Q_D + 2) * N + slot]},
               a.query[Q_TMAX * N + slot], (kind & 1) != 0);
   return true;
 }
@@ -1038,7 +1051,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
         // the hit being shaded (raytracer.cpp:293-303): the hit primitive's test with
         // attributes on the ray just traced (the query record), kept in the slot's hit record
         // for the shadow steps that follow
-        const QueryRec qr = load_query(a.query, N, slot);
+        const QueryRec qr = load_query(a.query, N, slot, a.cam.location);
         const Ray tr{qr.o, qr.d, qr.tq};
         const float4* rec = a.c.prims + (size_t)res_ld * a.c.prim_stride4;
         PrimA P;
@@ -1081,12 +1094,12 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
         if (light > 0) fin = V3{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
       } else if (st0 == ST_CLOSEST) {
         if (kFrames) {
-          const QueryRec qr = load_query(a.query, N, slot);
+          const QueryRec qr = load_query(a.query, N, slot, a.cam.location);
           ray.o = qr.o;
           ray.d = qr.d;
           ray.time = qr.tq;  // closest queries carry the ray time there
         } else if (!a.pinhole) {
-          ray.o = load_query(a.query, N, slot).o;
+          ray.o = load_query(a.query, N, slot, a.cam.location).o;
         } else {
           ray.o = cam_o;
         }
@@ -1414,7 +1427,8 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
     S[F_KEY * N + slot] = (uint32_t)rng.key;
     S[(F_KEY + 1) * N + slot] = (uint32_t)(rng.key >> 32);
   }
-  store_query(a.query, N, slot, ray.o, ray.d, ray.time, 0);
+  if (a.pinhole) store_cam_query(a.query, N, slot, ray.d, ray.time);
+  else store_query(a.query, N, slot, ray.o, ray.d, ray.time, 0);
   if (lane == __ffsll((long long)__ballot(1)) - 1) *a.any_query = 1u;
 }
 
@@ -2043,6 +2057,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
+  for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
   ta.light_samples = p->light_samples;
   // the closest hit starts its shade loop in the tracing lane too: planes, or untextured
   // transformed shapes (that lane computes point and normal, not (u, v)); RT_SOFT_START=0 off
