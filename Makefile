@@ -8,8 +8,11 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
 ARCH ?= gfx950
-# exact IEEE binary32: no FMA contraction, correctly rounded div/sqrt on the device
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fPIC -Wno-unused-result
+# exact IEEE binary32: no FMA contraction, correctly rounded div/sqrt on the device.
+# -fno-slp-vectorize: the SLP vectoriser paired scalar f32 ops into v_pk_add/v_pk_mul and built
+# the register pairs with moves (trace kernel 125 -> 84 VGPRs without it, 5 waves/SIMD fit;
+# headline +4 %, C4 +7 %: tools/exp_r02_61.sh).  The explicit f32x2 culling fma stays packed.
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -fPIC -Wno-unused-result
 CXXFLAGS := -O2 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-function
 LIB := ray_tracying_amd/lib
 BIN := ray_tracying_amd/bin
@@ -40,7 +43,7 @@ $(BIN)/raytracer: $(SRC)/host/main.cpp $(LIB)/librt_host.so $(LIB)/librt_comm.so
 variant: $(LIB)/librt_host.so
 	@mkdir -p ray_tracying_amd/lib_$(V)
 	$(HIPCC) $(HIPFLAGS) $(VDEFS) -shared $(SRC)/hip/rt_hip.hip -o ray_tracying_amd/lib_$(V)/librt_hip.so
-	cp $(LIB)/librt_host.so ray_tracying_amd/lib_$(V)/
+	cp $(LIB)/librt_host.so $(LIB)/librt_comm.so ray_tracying_amd/lib_$(V)/
 
 # Host code and oracle under AddressSanitizer + UndefinedBehaviorSanitizer (host only: the
 # GPU pool runs no sanitizers on device code).  Run the CPU suite against them with

@@ -649,7 +649,8 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #define RT_PT_FLUSH
 #endif
 #ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 4  // waves per SIMD the register allocation targets (A/B builds: make variant)
+#define RT_TRACE_WAVES 5  // waves per SIMD the register allocation targets (A/B builds: make variant);
+                          // 5 fits without spills once the SLP vectoriser is off (Makefile)
 #endif
 template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES, 8))) void trace_refill_kernel(TraceArgs ta) {

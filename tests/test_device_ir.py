@@ -19,7 +19,7 @@ def ir(tmp_path_factory):
         pytest.skip("hipcc not available")
     out = str(tmp_path_factory.mktemp("ir") / "rt.ll")
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                    "-fhip-fp32-correctly-rounded-divide-sqrt", "--cuda-device-only", "-emit-llvm", "-S",
+                    "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize", "--cuda-device-only", "-emit-llvm", "-S",
                     os.path.join(ROOT, "ray_tracying_amd", "csrc", "hip", "rt_hip.hip"), "-o", out],
                    check=True, capture_output=True)
     return open(out).read()
