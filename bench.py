@@ -51,7 +51,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 N_CU, VALU_WAVE_INSTR_PER_CU_CYCLE, MAX_CLOCK_GHZ = 256, 1, 2.4
 VALU_PEAK_TOPS = N_CU * VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3  # 39.3 T lane-ops/s
 NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
-PMC_PROFILE = "r02_v7"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r02_v8"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
