@@ -66,7 +66,7 @@ constexpr int kCtrStride = 32;
 constexpr int kMaxHostBatch = 16;
 // Slot pipelines: the slots are split into independent logic -> trace pipelines on their own
 // streams, so one pipeline's logic step and launch tail overlap the other's traversal.
-constexpr int kPipes = 2;
+constexpr int kPipes = 4;  // at most (RT_PIPES); the default is pipes_env()
 constexpr size_t kFetchLines = (size_t)kMaxFetchShards + 2;  // fetch counters + two any_query lines, per pipeline
 
 // ---------------------------------------------------------------- slot state (SoA, HBM)
@@ -1590,6 +1590,10 @@ void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, unsig
   if (count) launch_trace2<true>(ta, planes, soft, blocks, lds, st);
   else launch_trace2<false>(ta, planes, soft, blocks, lds, st);
 }
+static int pipes_env() {  // read per call: tests vary it within one process
+  const char* e = std::getenv("RT_PIPES");
+  return e ? std::max(1, std::min(kPipes, std::atoi(e))) : 2;
+}
 static int fetch_shards_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_FETCH_SHARDS");
@@ -2092,15 +2096,18 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const bool step_sync = diag || replay_iter >= 0;
 #endif
 
-  // ---- pipelines: the slots may split into kPipes independent logic -> trace sequences, one
-  // per stream (units are claimed from the shared batch counters, so the split changes no
-  // value): a pipeline's logic step and the tail of its trace launch then run while the other
-  // pipeline's traversal fills the machine.  Measured (same box, A/B): headline +0.8 %, one
-  // rank's share of an 8-way split -1 %, C4 (92 short steps) -5 %; so one pipeline unless
-  // RT_PIPES=2 asks for two.
-  int n_pipes = 1;
-  if (const char* e = std::getenv("RT_PIPES")) n_pipes = std::max(1, std::min(kPipes, std::atoi(e)));
-  if (step_sync || n_slots < kPipes * kBlock) n_pipes = 1;
+  // ---- pipelines: the slots split into independent logic -> trace sequences, one per stream
+  // (units are claimed from the shared batch counters, so the split changes no value): one
+  // pipeline's trace launch drains (its last waves finish their last rays) and its logic and
+  // start steps run while the other pipeline's traversal fills the machine.  Measured (r03,
+  // one box, RT_PIPES=1/2/3/4): headline 4967/5521/5337/5181 Mrays/s, C5 5869/6551/6428/6331,
+  // one rank's eighth 4306/4467/4282/4306, C3 19082/19769/18702/19094, C4 12656/13037/13461/
+  // 13518; a call of one launch (C2, 1 spp primary only: 1M units) 1462/1193 -- two pipelines
+  // by default, one for calls of at most 4M units (a second pipeline only adds a launch tail).
+  int n_pipes = n_units <= (4LL << 20) ? 1 : pipes_env();
+  if (const char* e = std::getenv("RT_PIPES")) n_pipes = pipes_env();  // an explicit request holds for any size
+  if (step_sync) n_pipes = 1;
+  n_pipes = std::max(1, std::min(n_pipes, n_slots / kBlock));  // every pipeline gets whole blocks of slots
   struct Pipe {
     LogicArgs la;
     TraceArgs ta;

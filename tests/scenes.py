@@ -200,6 +200,11 @@ def cases() -> dict:
         "blend_c3_antialiasing": (lambda: blend("Antialiasing", (64, 48)), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
         "blend_c4_glossy_soft": (lambda: blend("glossy_reflection", (64, 48), light_radius=1.0),
                                  dict(use_bvh=True, spp_sqrt=2, light_samples=2)),
+        # C3 / C4 at the bench's sample settings (-s 10 = 100 spp; C4 -light_sample 4, light radius
+        # 1), 128^2: SURVEY.md 8(c) parity chain item (4) at 100 spp
+        "blend_c3_s10": (lambda: blend("Antialiasing", (128, 128)), dict(use_bvh=True, spp_sqrt=10, light_samples=1)),
+        "blend_c4_s10": (lambda: blend("glossy_reflection", (128, 128), light_radius=1.0),
+                         dict(use_bvh=True, spp_sqrt=10, light_samples=4)),
         "blend_dop": (lambda: blend("dop"), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
         "blend_motion_blur": (lambda: blend("motion_blur"), dict(use_bvh=True, spp_sqrt=2, light_samples=1)),
         "blend_distributed": (lambda: blend("Distributed"), dict(use_bvh=True, spp_sqrt=1, light_samples=2)),

@@ -6,8 +6,8 @@ entries (every deeper entry spills to HBM), extreme refill / leaf-phase threshol
 many work-counter shards, a slot count so small that a frame takes dozens of steps, and the
 slots split into two pipelines on two streams, soft-shadow samples advanced by
 shadow_step_kernel or by the logic kernel instead of the tracing lane, the greedy BVH4
-collapse instead of the SAH-optimal one, and point-light shadow rays left unfused in a small
-call.
+collapse instead of the SAH-optimal one, point-light shadow rays left unfused in a small
+call, and one or four slot pipelines instead of the default two.
 """
 import os
 import subprocess
@@ -41,13 +41,14 @@ KNOBS = [
     {"RT_BATCH_SHARDS": "1024", "RT_FETCH_SHARDS": "1"},
     {"RT_BATCH_SHARDS": "1024", "RT_SLOTS": "4096"},  # more shards than slot-waves: clamped
     {"RT_MAX_UNITS": "3000"},  # the call runs as many tile chunks
-    {"RT_PIPES": "2"},  # two slot pipelines on two streams
     {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
     {"RT_SOFT_START": "0"},  # a closest hit's first shadow sample emitted by the logic step
     {"RT_SOFT_FUSE": "0"},  # soft-shadow samples advanced by shadow_step_kernel, not the tracing lane
     {"RT_SOFT_FUSE": "0", "RT_SHADOW_STEP": "0"},  # ... or by the logic kernel itself
     {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
     {"RT_FUSE": "0"},  # point-light shadow rays as their own queries (small calls fuse them by default)
+    {"RT_PIPES": "1"},  # one slot pipeline (the default is two on two streams)
+    {"RT_PIPES": "4", "RT_SLOTS": "8192"},  # four pipelines of two slot blocks each
 ]
 
 
