@@ -57,6 +57,8 @@ extern "C" {
  *   b[0..11]  object_to_world rows 0..2                      shapes.hpp:69
  * Plane (shapes.cpp:444-494; a triangle is a Plane with c3 == c0):
  *   a[0..2]=c0 a[3]=n.x  a[4..6]=c1 a[7]=n.y  a[8..10]=c2 a[11]=n.z  a[12..14]=c3 a[15]=tag
+ *   (with RT_TAG_TRI1_NEVER: c3 = c0 and a[12] is a squared radius, finite and >= 0 -- only on
+ *   a Plane record with RT_TAG_PLANE_VALID; rt_scene_create rejects any other use of the bit)
  *   n = normalize(cross(c1-c0, c2-c0)), computed on the host with the reference's ops.
  * Records are stored in traversal order; rt_prim_ref gives each one's reference order. */
 typedef struct rt_prim {

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -170,7 +171,8 @@ struct LogicArgs {
   int spp_sqrt, light_samples;
   uint64_t seed_key;
   // work
-  const int* tile_ids;
+  const int* tile_ids;         // the call's tiles in render order (costliest first, see tile_cost_order)
+  const int* tile_out;         // render-order index -> the caller's index (output position); null: identity
   int tile_affine;            // tile_ids[i] == tile_first + i * tile_step (no table lookup)
   int tile_first, tile_step;
   int tile_w, tile_h, tiles_x, sub_x;
@@ -666,8 +668,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
   const unsigned int any = *ta.any_query;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ta.host_flag = any;  // read by the host after the step
   if (any == 0u) return;
+  // the work queue: 64-slot groups, dealt to fetch_shards counters round robin (group g to
+  // shard g % shards), so the queue is consumed in slot order -- the call's costliest tiles
+  // first (tile_cost_order) -- and the launch ends on cheap rays
   const unsigned nfs = (unsigned)ta.fetch_shards;
-  const unsigned shard_len = (((nq + nfs - 1) / nfs) + 63u) & ~63u;
+  const unsigned n_groups = (nq + 63u) >> 6;
   // wave-uniform work queue: [q_next, q_end)
   int sk = 0;
   unsigned q_next = 0, q_end = 0;
@@ -830,16 +835,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_TRACE
         if (q_next >= q_end) {  // next 64 slots: this shard's counter, then the other shards'
           for (;;) {
             const int sh = (int)((blockIdx.x + sk) % nfs);
-            const unsigned st0 = (unsigned)sh * shard_len;
-            const unsigned len = st0 < nq ? min(shard_len, nq - st0) : 0u;
-            unsigned base = 0;
-            if (len > 0) {
-              if (lane == 0) base = atomicAdd(ta.fetch + sh * kFetchStride, 64u);
-              base = __shfl(base, 0);
+            unsigned j = 0;
+            if ((unsigned)sh < n_groups) {
+              if (lane == 0) j = atomicAdd(ta.fetch + sh * kFetchStride, 1u);
+              j = __shfl(j, 0);
             }
-            if (len > 0 && base < len) {
-              q_next = (unsigned)ta.slot_base + st0 + base;
-              q_end = (unsigned)ta.slot_base + st0 + min(base + 64u, len);
+            const unsigned g = (unsigned)sh + j * nfs;
+            if ((unsigned)sh < n_groups && g < n_groups) {
+              q_next = (unsigned)ta.slot_base + g * 64u;
+              q_end = (unsigned)ta.slot_base + min(g * 64u + 64u, nq);
               // 64-slot groups are slot-waves of the logic step: skip one whose slots retired
               if (a.wave_done[q_next >> 6] != 0u) continue;
               break;
@@ -968,7 +972,8 @@ __device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, 
   const int tid = a.tile_affine ? a.tile_first + tl * a.tile_step : a.tile_ids[tl];
   x = (tid % a.tiles_x) * a.tile_w + lx;
   y = (tid / a.tiles_x) * a.tile_h + ly;
-  out_off = ((size_t)tl * tile_px + (size_t)ly * a.tile_w + lx) * 3;
+  const int to = a.tile_out ? a.tile_out[tl] : tl;
+  out_off = ((size_t)to * tile_px + (size_t)ly * a.tile_w + lx) * 3;
   return x < a.cam.res_x && y < a.cam.res_y;
 }
 
@@ -1393,7 +1398,12 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
     if (lane == 0) a.wave_done[wave] = 1u;
     return;
   }
-  if (lane == 0) a.wave_done[wave] = 0u;
+  if (lane == 0) {
+    a.wave_done[wave] = 0u;
+    // another step is needed even if every pixel of the batch lies outside the image (an edge
+    // tile's bottom rows): the wave's slots stay idle, and the next step claims again
+    *a.any_query = 1u;
+  }
   int px, py, sample;
   if (!unit_coords(a, unit, px, py, sample)) {  // edge tile: pixel outside the image (stays idle)
     if (a.first_step) {
@@ -1430,7 +1440,6 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
   }
   if (a.pinhole) store_cam_query(a.query, N, slot, ray.d, ray.time);
   else store_query(a.query, N, slot, ray.o, ray.d, ray.time, 0);
-  if (lane == __ffsll((long long)__ballot(1)) - 1) *a.any_query = 1u;
 }
 
 // The next soft-shadow sample of a light (shade, raytracer.cpp:214-236): a slot in ST_SHADOW
@@ -1594,6 +1603,7 @@ static int pipes_env() {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_PIPES");
   return e ? std::max(1, std::min(kPipes, std::atoi(e))) : 2;
 }
+
 static int fetch_shards_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_FETCH_SHARDS");
@@ -1700,6 +1710,11 @@ struct rt_scene_s {
   hipEvent_t ev_a[kPipes][kMaxHostBatch] = {}, ev_b[kPipes][kMaxHostBatch] = {};
   hipStream_t aux[kPipes] = {};  // pipelines 1.. run on these non-blocking streams (0: the caller's)
   int last_iters = 0;  // steps the previous render took: the size of the next render's first host batch
+  // tile cost model (tile_cost_order): a sample of primitive centres, and the per-tile cost of
+  // the last camera / tile size it was projected for
+  std::vector<float> cost_pts;
+  std::vector<unsigned char> cost_key;
+  std::vector<float> tile_cost;
   int fuse_lights = 0;  // > 0: point lights whose shadow rays the trace kernel may fuse (see rt_scene_create)
 };
 
@@ -1715,6 +1730,44 @@ static void free_workspace(rt_scene_s* s) {
   s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr; s->d_hit = nullptr;
   s->slots_cap = 0;
   s->samples_cap = 0;
+}
+
+// Render order of a call's tiles: costliest first.  A launch ends when its slowest rays do,
+// so the work consumed last should be cheap: the tiles are ordered by a cost estimate --
+// how many primitives (a sample of their centres) project into the tile -- so the
+// background tiles come last, in every launch and at the end of the call.  Scheduling only:
+// every sample is keyed by its pixel (counter RNG), so the order changes no value.  The
+// per-tile costs are cached per camera and tile size.
+static void tile_cost_order(rt_scene_s* s, const rt_camera_desc* cam, int tile_w, int tile_h, int tiles_x, int tiles_y,
+                            const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
+  order.resize((size_t)n_tiles);
+  for (int i = 0; i < n_tiles; ++i) order[i] = i;
+  if (const char* e = std::getenv("RT_TILE_ORDER")) wanted = std::atoi(e) != 0;  // 0 / 1: never / always
+  if (!wanted || n_tiles < 2 || s->cost_pts.empty()) return;
+  std::vector<unsigned char> key(sizeof(rt_camera_desc) + 2 * sizeof(int));
+  std::memcpy(key.data(), cam, sizeof(rt_camera_desc));
+  std::memcpy(key.data() + sizeof(rt_camera_desc), &tile_w, sizeof(int));
+  std::memcpy(key.data() + sizeof(rt_camera_desc) + sizeof(int), &tile_h, sizeof(int));
+  if (key != s->cost_key) {
+    s->cost_key = key;
+    s->tile_cost.assign((size_t)tiles_x * tiles_y, 0.0f);
+    const float* L = cam->location;
+    for (size_t k = 0; k + 2 < s->cost_pts.size(); k += 3) {
+      const float v[3] = {s->cost_pts[k] - L[0], s->cost_pts[k + 1] - L[1], s->cost_pts[k + 2] - L[2]};
+      const float c = v[0] * cam->z_dir[0] + v[1] * cam->z_dir[1] + v[2] * cam->z_dir[2];
+      if (!(c > 1e-6f)) continue;  // behind the camera
+      const float a = v[0] * cam->x_dir[0] + v[1] * cam->x_dir[1] + v[2] * cam->x_dir[2];
+      const float b = v[0] * cam->y_dir[0] + v[1] * cam->y_dir[1] + v[2] * cam->y_dir[2];
+      // camera_ray's mapping inverted: n = 1 - 2 p / res, n * half_sensor = (a / c) * focal
+      const float px = (1.0f - a / c * cam->focal_length / cam->half_sensor_w) * 0.5f * (float)cam->res_x;
+      const float py = (1.0f - b / c * cam->focal_length / cam->half_sensor_h) * 0.5f * (float)cam->res_y;
+      if (!(px >= 0.0f && py >= 0.0f && px < (float)cam->res_x && py < (float)cam->res_y)) continue;
+      s->tile_cost[(size_t)((int)py / tile_h) * tiles_x + (int)px / tile_w] += 1.0f;
+    }
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int i, int j) {
+    return s->tile_cost[(size_t)tile_ids[i]] > s->tile_cost[(size_t)tile_ids[j]];
+  });
 }
 
 extern "C" {
@@ -1812,6 +1865,16 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
       if (!ok) return fail(RT_EINVAL, "rt_scene_create: node child out of range");
     }
   }
+  // RT_TAG_TRI1_NEVER changes what a[12] means (a squared radius, not c3.x): only on a valid
+  // Plane record, with a finite non-negative radius
+  for (int32_t i = 0; i < d->n_prims; ++i) {
+    const float* a = reinterpret_cast<const float*>(d->prims) + (size_t)i * (d->prim_stride / 4);
+    uint32_t tag;
+    std::memcpy(&tag, a + 15, 4);
+    if ((tag & RT_TAG_TRI1_NEVER) &&
+        !(RT_TAG_KIND(tag) == RT_PRIM_PLANE && (tag & RT_TAG_PLANE_VALID) && std::isfinite(a[12]) && a[12] >= 0.0f))
+      return fail(RT_EINVAL, "rt_scene_create: RT_TAG_TRI1_NEVER on a record that is not a valid Plane with a[12] >= 0");
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
     return fail(RT_ENODEV, "rt_scene_create: no such HIP device");
@@ -1875,6 +1938,27 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     if (const char* e = std::getenv("RT_TRACE_BPC")) bpc = std::max(1, std::min(bpc, std::atoi(e)));  // diagnostic
     s->n_cu = ncu;
     s->trace_blocks_per_cu = bpc;
+  }
+  {  // tile cost model: up to 64K primitive centres (planes: the mean of c0, c1, c2; transformed
+     // shapes: the object-to-world translation)
+    const int32_t n = d->n_prims;
+    const int32_t stride = std::max(1, n / 65536);
+    const float* P = reinterpret_cast<const float*>(d->prims);
+    const size_t w = (size_t)d->prim_stride / 4;
+    for (int32_t i = 0; i < n; i += stride) {
+      const float* a = P + (size_t)i * w;
+      uint32_t tag;
+      std::memcpy(&tag, a + 15, 4);
+      if (d->prim_stride == 64 || RT_TAG_KIND(tag) == RT_PRIM_PLANE) {
+        s->cost_pts.push_back((a[0] + a[4] + a[8]) / 3.0f);
+        s->cost_pts.push_back((a[1] + a[5] + a[9]) / 3.0f);
+        s->cost_pts.push_back((a[2] + a[6] + a[10]) / 3.0f);
+      } else {
+        s->cost_pts.push_back(a[16 + 3]);
+        s->cost_pts.push_back(a[16 + 7]);
+        s->cost_pts.push_back(a[16 + 11]);
+      }
+    }
   }
   s->desc.prims = nullptr; s->desc.nodes = nullptr; s->desc.materials = nullptr; s->desc.prim_refs = nullptr;
   s->desc.ref_leaf_boxes = nullptr;
@@ -1946,12 +2030,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   long long slots = slot_cap;
   if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
   const int n_slots = (int)(((std::min<long long>(n_units, slots) + kBlock - 1) / kBlock) * kBlock);
-  if ((size_t)n_tiles > s->tiles_cap) {
+  if ((size_t)n_tiles > s->tiles_cap) {  // render-order tile ids, then their output positions
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     s->d_tiles = nullptr;
     s->tiles_cap = 0;
     s->tiles_on_device.clear();
-    HIP_TRY(hipMalloc(&s->d_tiles, (size_t)n_tiles * sizeof(int32_t)), RT_ENOMEM);
+    HIP_TRY(hipMalloc(&s->d_tiles, (size_t)n_tiles * 2 * sizeof(int32_t)), RT_ENOMEM);
     s->tiles_cap = (size_t)n_tiles;
   }
   if ((size_t)n_slots > s->slots_cap || (need_frames && !s->d_frames) || (need_refr && !s->d_refr)) {
@@ -1975,11 +2059,24 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_samples, (size_t)n_units * 3 * sizeof(float)), RT_ENOMEM);
     s->samples_cap = (size_t)n_units * 3;
   }
-  // the tile list is uploaded only when it changed (a renderer's frames reuse one list)
-  if (s->tiles_on_device.size() != (size_t)n_tiles ||
-      !std::equal(tile_ids, tile_ids + n_tiles, s->tiles_on_device.begin())) {
-    s->tiles_on_device.assign(tile_ids, tile_ids + n_tiles);
-    HIP_TRY(hipMemcpyAsync(s->d_tiles, s->tiles_on_device.data(), (size_t)n_tiles * sizeof(int32_t),
+  // render order and the tile list in that order + output positions; uploaded only when it
+  // changed (a renderer's frames reuse one list).  Costliest tiles first for a call whose
+  // samples are all in flight at once (one step per pipeline: one rank's share of a split
+  // frame), where the call's last drain is exposed: one rank's eighth of the headline frame
+  // 4509-4564 -> 4723-4727 Mrays/s.  Longer calls keep the caller's order (whole frames,
+  // C4, C5: within -1.6 %..+0 % -- the other pipeline hides their drains).
+  std::vector<int32_t> order;
+  tile_cost_order(s, cam, tile_w, tile_h, tiles_x, tiles_y, tile_ids, n_tiles, n_units <= n_slots, order);
+  std::vector<int32_t> tl_dev((size_t)n_tiles * 2);
+  bool identity = true;
+  for (int i = 0; i < n_tiles; ++i) {
+    tl_dev[i] = tile_ids[order[i]];
+    tl_dev[(size_t)n_tiles + i] = order[i];
+    identity = identity && order[i] == i;
+  }
+  if (s->tiles_on_device != tl_dev) {
+    s->tiles_on_device = tl_dev;
+    HIP_TRY(hipMemcpyAsync(s->d_tiles, s->tiles_on_device.data(), tl_dev.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice, stream), RT_EDEVICE);
   }
   unsigned int* ctl = (unsigned int*)s->d_ctl;  // cleared by init_kernel
@@ -2003,11 +2100,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.light_samples = p->light_samples;
   la.seed_key = mix64_host(p->seed + 0x9E3779B97F4A7C15ull);
   la.tile_ids = s->d_tiles;
+  la.tile_out = identity ? nullptr : s->d_tiles + n_tiles;
   // affine tile lists (one GPU: 0, 1, 2 ...; round-robin ranks: r, r + N ...) need no lookup
-  la.tile_first = tile_ids[0];
-  la.tile_step = n_tiles > 1 ? tile_ids[1] - tile_ids[0] : 1;
+  la.tile_first = tl_dev[0];
+  la.tile_step = n_tiles > 1 ? tl_dev[1] - tl_dev[0] : 1;
   la.tile_affine = 1;
-  for (int i = 0; i < n_tiles && la.tile_affine; ++i) la.tile_affine = tile_ids[i] == la.tile_first + i * la.tile_step;
+  for (int i = 0; i < n_tiles && la.tile_affine; ++i) la.tile_affine = tl_dev[i] == la.tile_first + i * la.tile_step;
   la.tile_w = tile_w;
   la.tile_h = tile_h;
   la.tiles_x = tiles_x;

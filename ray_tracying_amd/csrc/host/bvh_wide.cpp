@@ -24,8 +24,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <system_error>
+#include <thread>
 #include <utility>
 #include <stdexcept>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -129,14 +132,19 @@ struct BuildOut {
   }
 };
 
-// Run fn(chunk, begin, end) over `n` items in `chunks` contiguous chunks on their own threads.
+// Run fn(chunk, begin, end) over `n` items in `chunks` contiguous chunks on their own threads
+// (a chunk whose thread cannot be created runs on the calling thread).
 template <class F>
 static void parallel_chunks(size_t n, int chunks, F&& fn) {
   std::vector<std::thread> th;
   const size_t per = (n + chunks - 1) / chunks;
   for (int c = 1; c < chunks; ++c) {
     const size_t b = std::min(n, c * per), e = std::min(n, (c + 1) * per);
-    th.emplace_back([&fn, c, b, e] { fn(c, b, e); });
+    try {
+      th.emplace_back([&fn, c, b, e] { fn(c, b, e); });
+    } catch (const std::system_error&) {
+      fn(c, b, e);
+    }
   }
   fn(0, 0, std::min(n, per));
   for (auto& t : th) t.join();
@@ -323,8 +331,11 @@ struct SAHBuilder {
       make_leaf(out, id, refs);
       return id;
     }
-    const bool wide = (size_t)n >= kChunkMin && threads > 1;
-    const int chunks = wide ? threads : 1;
+    // chunk threads are bounded by the idle build threads (subtrees running on spawned threads
+    // hold the others), so the process never runs much more than `threads` threads at once
+    const int idle = 1 + std::max(0, spare.load());
+    const bool wide = (size_t)n >= kChunkMin && threads > 1 && idle > 1;
+    const int chunks = wide ? std::min(threads, idle) : 1;
     // object split: binned SAH over all three axes
     ObjBins ob;
     if (wide) {
@@ -475,9 +486,14 @@ struct SAHBuilder {
                        spare.compare_exchange_strong(tok, tok - 1);
     if (spawn) {  // left subtree on another thread, right here; appended in DFS order
       BuildOut lo, ro;
-      std::thread t([&] { build(std::move(L), depth + 1, bl, lo); });
+      std::thread t;
+      try {
+        t = std::thread([&] { build(std::move(L), depth + 1, bl, lo); });
+      } catch (const std::system_error&) {  // no thread: the left subtree runs here first
+        build(std::move(L), depth + 1, bl, lo);
+      }
       build(std::move(R), depth + 1, br, ro);
-      t.join();
+      if (t.joinable()) t.join();
       spare.fetch_add(1);
       l = (int)out.nodes.size();
       out.append(std::move(lo));

@@ -456,9 +456,10 @@ void BuildTimer::lap(const char* phase) {
 }
 
 int build_threads() {
-  if (const char* e = std::getenv("RT_BUILD_THREADS")) return std::max(1, std::min(256, std::atoi(e)));
   const unsigned hc = std::thread::hardware_concurrency();
-  return std::max(1, std::min(16, (int)(hc ? hc : 1)));
+  const int cores = std::max(1, (int)(hc ? hc : 1));
+  if (const char* e = std::getenv("RT_BUILD_THREADS")) return std::max(1, std::min(std::min(64, cores), std::atoi(e)));
+  return std::min(16, cores);
 }
 
 namespace {

@@ -107,3 +107,15 @@ def test_device_quantise_matches_host(gpu):
     rt.quantise_device(d.data_ptr(), vals.size, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), rt.quantise(vals))
+
+
+def test_lockstep_batches_past_the_image_edge(tmp_path, gpu, monkeypatch):
+    """with no lights every sample finishes in one step, so a slot-wave's 64
+    samples finish together; with few slots (RT_SLOTS=4096) and a width that is not a multiple
+    of the 64-pixel tile, some steps claim only batches whose pixels all lie outside the image
+    (the right edge tile's padding columns).  Such a claim must still keep the frame going --
+    no batch may be left unclaimed and no pixel read from stale samples."""
+    monkeypatch.setenv("RT_SLOTS", "4096")
+    monkeypatch.setenv("RT_PIPES", "1")
+    p = scenes.write(scenes.soup(600, seed=3, res=(72, 40), light=False), str(tmp_path / "s.json"))
+    check(p, use_bvh=True, spp_sqrt=10, light_samples=1)

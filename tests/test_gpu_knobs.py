@@ -7,7 +7,8 @@ many work-counter shards, a slot count so small that a frame takes dozens of ste
 slots split into two pipelines on two streams, soft-shadow samples advanced by
 shadow_step_kernel or by the logic kernel instead of the tracing lane, the greedy BVH4
 collapse instead of the SAH-optimal one, point-light shadow rays left unfused in a small
-call, and one or four slot pipelines instead of the default two.
+call, one or four slot pipelines instead of the default two, and the tiles rendered in the
+caller's order instead of costliest first (small calls' default).
 """
 import os
 import subprocess
@@ -48,6 +49,7 @@ KNOBS = [
     {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
     {"RT_FUSE": "0"},  # point-light shadow rays as their own queries (small calls fuse them by default)
     {"RT_PIPES": "1"},  # one slot pipeline (the default is two on two streams)
+    {"RT_TILE_ORDER": "0"},  # tiles in the caller's order (small calls render costliest tiles first)
     {"RT_PIPES": "4", "RT_SLOTS": "8192"},  # four pipelines of two slot blocks each
 ]
 

@@ -132,3 +132,40 @@ def test_render_without_gpu_fails_loudly(tmp_path):
     sc = rt.Scene(path)
     with pytest.raises(rt.NativeError):
         sc.render()
+
+
+def test_scene_create_rejects_misused_tri1_never_tag(tmp_path):
+    """RT_TAG_TRI1_NEVER turns a[12] into a squared radius; rt_scene_create must
+    reject the bit on anything but a valid Plane record with a finite a[12] >= 0.  The check
+    runs before any device call, so it holds on a machine without a GPU too."""
+    rt._load()
+    sc = rt.Scene(scenes.write(scenes.soup(300, seed=2), str(tmp_path / "s.json")))
+    d = sc.desc()
+    w = d.prim_stride // 4
+    prims = np.ctypeslib.as_array(ctypes.cast(d.prims, ctypes.POINTER(ctypes.c_float)), shape=(d.n_prims * w,))
+    recs = prims.reshape(d.n_prims, w).copy()
+    tags = recs[:, 15].view(np.uint32)
+    tri1 = np.flatnonzero(tags & 16)
+    assert len(tri1) > 0, "the soup's triangles carry RT_TAG_TRI1_NEVER"
+    k = int(tri1[0])
+
+    def create(bad):
+        dd = rt.rt_scene_desc.from_buffer_copy(d)
+        dd.prims = bad.ctypes.data
+        h = ctypes.c_void_p()
+        rc = rt._hip.rt_scene_create(0, ctypes.byref(dd), ctypes.byref(h))
+        if rc == 0:
+            rt._hip.rt_scene_destroy(h)
+        return rc, rt._hip.rt_last_error().decode()
+
+    for mutate in (lambda r: r.__setitem__((k, 12), -1.0),                      # negative radius
+                   lambda r: r.__setitem__((k, 12), np.float32("nan")),         # NaN radius
+                   lambda r: r[k, 15:16].view(np.uint32).__iand__(np.uint32(~4 & 0xffffffff)),  # not a valid plane
+                   lambda r: r[k, 15:16].view(np.uint32).__iand__(np.uint32(~3 & 0xffffffff))):  # kind: sphere
+        bad = recs.copy()
+        mutate(bad)
+        rc, msg = create(bad)
+        assert rc == -1 and "TRI1_NEVER" in msg, (rc, msg)
+    rc, msg = create(recs.copy())  # the untouched records pass the check (then need a device)
+    assert "TRI1_NEVER" not in msg
+    sc.close()
