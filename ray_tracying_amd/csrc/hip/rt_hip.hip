@@ -1607,7 +1607,7 @@ static int pipes_env() {  // read per call: tests vary it within one process
 static int fetch_shards_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_FETCH_SHARDS");
-    return e ? std::max(1, std::min(kMaxFetchShards, std::atoi(e))) : 8;
+    return e ? std::max(1, std::min(kMaxFetchShards, std::atoi(e))) : 32;  // r03 sweep: 4 / 8 / 16 / 32: 5377 / 5542 / 5628 / 5769 (headline)
   }();
   return v;
 }
@@ -1621,7 +1621,7 @@ static int batch_shards_env() {
 static int leaf_min_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_LEAF_MIN");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : 16;
+    return e ? std::max(1, std::min(64, std::atoi(e))) : 24;  // r03 sweep at 32M slots: 12 / 16 / 24 / 32 (two pipelines)
   }();
   return v;
 }
@@ -2021,13 +2021,17 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const long long n_units = (long long)n_pixels * n_samples;
   if (n_units > 0x7ffffff0LL) return fail(RT_EINVAL, "rt_render_tiles: too many samples in one call (split the tiles)");
   // whole blocks of slots; a wave renders 64 consecutive samples per batch
-  // Slots in flight: every sample of the call up to 16M (measured with the refill trace kernel,
-  // 1024^2 x 100 spp soup: the whole frame (105M samples) 16M = 26M > 33M; one rank's share of
-  // an 8-way split (13M) all in flight 3370 vs 6.5M 3081 vs 3.3M 2742 Mrays/s; 4-way (26M) 16M
-  // 3726 vs 6.5M 3552; 2-way (52M) 16M 4048 vs 13M 3944).  Fewer slots means more, shorter
-  // steps, each ending in a launch tail; more than 16M only adds idle slots to every logic step.
-  const long long slot_cap = std::min(n_units, 1LL << 24);
-  long long slots = slot_cap;
+  // Slots in flight (r03 sweep, two pipelines, one box; Mrays/s): every sample of a call of at
+  // most 32M units (one rank's quarter of the headline frame, 26M: 4913 at 16M slots -> 5211 all
+  // in flight); larger calls 0.45 of their units, between 32M and 96M (headline 105M units:
+  // 16M 5554, 40M 5756, 48M 5835, 52M 5458 -- at half the frame each pipeline's steps fall into
+  // lockstep and the drains coincide; C5 1.07G units: 16M 6630, 48M 7157, 96M 7290; C3 16M
+  // 19547, 52M 20348); scenes with reflection / refraction keep 16M (C4 16M 13680, 52M 13023:
+  // their slots carry the Trace frames and take many short steps).
+  const bool frames_scene = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
+  long long slots = n_units <= (32LL << 20) ? n_units
+                    : frames_scene          ? (16LL << 20)
+                                            : std::max(32LL << 20, std::min(96LL << 20, n_units * 45 / 100));
   if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
   const int n_slots = (int)(((std::min<long long>(n_units, slots) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {  // render-order tile ids, then their output positions
