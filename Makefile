@@ -11,7 +11,7 @@ ARCH ?= gfx950
 # exact IEEE binary32: no FMA contraction, correctly rounded div/sqrt on the device.
 # -fno-slp-vectorize: the SLP vectoriser paired scalar f32 ops into v_pk_add/v_pk_mul and built
 # the register pairs with moves (trace kernel 125 -> 84 VGPRs without it, 5 waves/SIMD fit;
-# headline +4 %, C4 +7 %: tools/exp_r02_61.sh).  The explicit f32x2 culling fma stays packed.
+# headline +4 %, C4 +7 %, round 2 A/B).  The explicit f32x2 culling fma stays packed.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-slp-vectorize -fPIC -Wno-unused-result
 CXXFLAGS := -O2 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-function
 LIB := ray_tracying_amd/lib

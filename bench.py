@@ -44,26 +44,76 @@ sys.path.insert(0, ROOT)
 METRIC = "Mrays/sec (primary+secondary), 1024x1024 @100spp; % HBM roofline"
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate over 8 XCDs
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-# VALU peak: one wave64 VALU instruction per CU-cycle (4 SIMDs, one every 4 cycles each) --
-# measured on the box (tools/ubench_valu.hip, profiles/r02_ubench_valu.txt: independent
-# v_fma_f32 / v_max3_f32 / v_perm_b32 / v_pk_fma_f32 streams saturate at 0.84-0.90 per
-# CU-cycle at 2.4 GHz, 8 waves per SIMD); the guide's 2-cycle SIMD-32 issue is not reached
-N_CU, VALU_WAVE_INSTR_PER_CU_CYCLE, MAX_CLOCK_GHZ = 256, 1, 2.4
-VALU_PEAK_TOPS = N_CU * VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3  # 39.3 T lane-ops/s
+# VALU peaks (T lane-ops/s = wave64 instructions per CU-cycle x 256 CUs x 64 lanes x 2.4 GHz):
+#   measured -- the highest rate SQ_INSTS_VALU shows for tools/ubench_valu.hip's independent
+#     instruction streams (rocprofv3 --pmc, tools/pmc_ubench.py; profiles/<label>_ubench_valu_pmc.json)
+#   spec     -- MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles on a SIMD-32,
+#     4 SIMDs per CU = 2 instructions per CU-cycle (78.6 T lane-ops/s)
+N_CU, MAX_CLOCK_GHZ = 256, 2.4
+SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE = 2.0
+UBENCH_PROFILE = "r03_v4"  # committed counter-measured VALU microbenchmark (profiles/)
+
+
+def valu_peak(path):
+    """(wave64 VALU instructions per CU-cycle, source) from a pmc_ubench.py summary."""
+    if path and os.path.exists(path):
+        d = json.load(open(path))
+        if d.get("max_valu_wave_instr_per_cu_cycle"):
+            return float(d["max_valu_wave_instr_per_cu_cycle"]), f"{os.path.relpath(path, ROOT)} ({d.get('label', '')})"
+    return 1.0, "assumed 1 wave64 instruction per CU-cycle (no counter-measured microbenchmark found)"
 NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
-PMC_PROFILE = "r02_v8"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r03_v4"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def usable_cpus() -> int:
-    """Cores this process may run on (the job's CPU share; os.cpu_count() is the whole host)."""
+def cpu_quota():
+    """The job's CPU quota from its cgroup (v2 cpu.max, or v1 cfs quota / period) in cores, with
+    the file it came from; (None, None) when no quota is set."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return float(q) / float(per), path
+        except (OSError, ValueError):
+            pass
     try:
-        return len(os.sched_getaffinity(0))
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0 and per > 0:
+            return q / per, "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
+def usable_cpus() -> int:
+    """Cores this process may run on: its affinity mask, capped by the cgroup CPU quota (the
+    job's share; os.cpu_count() is the whole host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q, _ = cpu_quota()
+    if q is not None:
+        n = max(1, min(n, int(q)))
+    return n
+
+
+def host_cpus() -> dict:
+    """Where the multi-process CPU baseline's core count comes from (BENCH line evidence)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    q, src = cpu_quota()
+    return {"affinity": aff, "os_cpu_count": os.cpu_count(), "cgroup_quota_cores": q, "cgroup_quota_file": src,
+            "usable": usable_cpus(),
+            "rule": "usable = affinity capped by the cgroup quota; processes = min(16, usable) (the job's "
+                    "OMP_NUM_THREADS-style share on the GPU pool is 16)",
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def parse():
@@ -88,14 +138,18 @@ def parse():
     ap.add_argument("--primary-only", action="store_true",
                     help="SURVEY.md 8(d) C2 BVH-stress variant: the soup without lights (one ray per sample)")
     ap.add_argument("--cpu-procs", type=int, default=min(16, usable_cpus()),
-                    help="concurrent reference processes for the multi-core CPU figure (<= 1: skip); default: "
-                         "16 (the GPU box's CPU share per job) or fewer if fewer cores are usable")
+                    help="concurrent reference processes for the multi-core CPU figure (<= 1: skip); default: one "
+                         "per usable core (affinity capped by the cgroup CPU quota), at most 16 (the GPU pool's "
+                         "per-job share: OMP_NUM_THREADS / MAX_JOBS are 16 there)")
     ap.add_argument("--pmc-traffic", default=None,
                     help="JSON with per-launch HBM bytes of the trace kernel (tools/pmc_traffic.py); default: the "
                          "committed profile of the headline workload, attached to that workload only")
     ap.add_argument("--pmc-valu", default=None,
                     help="JSON with the trace kernel's VALU issue fraction / lane utilisation (tools/pmc_valu.py); "
                          "default as --pmc-traffic")
+    ap.add_argument("--ubench", default=None,
+                    help="JSON of the counter-measured VALU microbenchmark (tools/pmc_ubench.py): the measured VALU "
+                         "peak; default: the committed profile")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")
     return ap.parse_args()
@@ -160,10 +214,9 @@ def cpu_baseline(scene_path: str, args, rank: int):
             total += stk["rays"]
         out["value_multi_proc"] = sum(rates)
         out["procs"] = n
-        out["host_cpus"] = {"affinity": usable_cpus(), "os_cpu_count": os.cpu_count(),
-                            "note": "the GPU pool grants a job 16 host cores whatever the host exposes"}
-        out["sample_multi_proc"] = (f"{n} concurrent single-threaded processes (the job's 16-core CPU share), {band} rows "
-                                    f"each ({total} rays); value = sum of the per-process rates")
+        out["host_cpus"] = host_cpus()
+        out["sample_multi_proc"] = (f"{n} concurrent single-threaded processes (one per usable core, at most 16), "
+                                    f"{band} rows each ({total} rays); value = sum of the per-process rates")
     return out
 
 
@@ -264,11 +317,13 @@ def main():
     t0 = time.perf_counter()
     rays = 0
     trace_ms = 0.0
+    busy_ms = 0.0
     launches = 0
     for k in range(args.steps):
         st = step(args.seed + k)
         rays += st.rays
         trace_ms += st.trace_ms
+        busy_ms += st.trace_busy_ms
         launches += st.iterations
     torch.cuda.synchronize()
     if dist:
@@ -276,13 +331,13 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    tot = torch.tensor([float(rays), trace_ms, float(launches), bytes_per_ray * rays], dtype=torch.float64,
+    tot = torch.tensor([float(rays), trace_ms, float(launches), bytes_per_ray * rays, busy_ms], dtype=torch.float64,
                        device=coll)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=coll)
     if dist:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    rays_all, trace_ms_all, launches_all, alg_bytes_all = tot.tolist()
+    rays_all, trace_ms_all, launches_all, alg_bytes_all, busy_ms_all = tot.tolist()
     elapsed = tmax.item()
 
     if rank == 0 and dist:  # sanity: the gathered frame has every pixel, all finite
@@ -306,6 +361,12 @@ def main():
     avg_launch_ms = trace_ms_all / max(launches_all, 1)
     avg_launch_bytes = alg_bytes_all / max(launches_all, 1)
     alg_rate = avg_launch_bytes / (avg_launch_ms * 1e-3) / 1e9
+    # the slot pipelines' trace launches overlap (two streams), so a launch's HIP-event time
+    # includes time it shares the GPU with the other pipeline's: per launch the rate reads low.
+    # busy = the union of the launches' intervals (rt_stats.trace_busy_ms): per-frame bytes over
+    # it is the kernel's rate on the GPU
+    busy_ms_step = busy_ms_all / world / args.steps
+    alg_rate_busy = alg_bytes_all / world / args.steps / (busy_ms_step * 1e-3) / 1e9 if busy_ms_step > 0 else None
     # PMC summaries of the headline workload measured by rocprofv3 on this build
     # (tools/pmc_traffic.py, tools/pmc_valu.py; label = the build they were measured on).
     # They describe the headline frame only, so they are never attached to another line.
@@ -323,37 +384,53 @@ def main():
         pv = json.load(open(pmc_valu))
     kernel = {
         "kernel": "trace_refill_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
-        "launches_per_step": int(launches_all / args.steps),
-        "trace_share_of_step": round(trace_ms_all / world / (elapsed * 1e3), 3),
+        "launches_per_step": int(launches_all / args.steps / world),
+        "trace_busy_ms_per_step": round(busy_ms_step, 3),
+        "trace_share_of_step": round(busy_ms_step / (elapsed / args.steps * 1e3), 3),
+        "launch_timing": "HIP events on each slot pipeline's stream; two pipelines overlap their launches, so "
+                         "avg_launch_ms includes time shared with the other pipeline's launch (rocprofv3 agrees: "
+                         "profiles/<label>_kernel_stats.csv); trace_busy_ms_per_step is the union of the launches",
     }
     if args.scene:  # C1-C4: a few primitives, LDS/L1-resident -- no roofline claim
         roofline = {"bound": None, "frac": None, "achieved": None, "peak": None, "unit": None, "traffic": None,
                     "note": "scene of a few primitives (on-die): no roofline claim (SURVEY.md 8(d))", **kernel}
     else:
         valu = None
+        peak_ipc, peak_src = valu_peak(args.ubench or os.path.join(ROOT, "profiles", UBENCH_PROFILE + "_ubench_valu_pmc.json"))
+        peak_tops = N_CU * peak_ipc * 64 * MAX_CLOCK_GHZ / 1e3
+        spec_tops = N_CU * SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3
         if pv:
             # useful lane-ops/s = wave64 VALU instructions/s x 64 x lane utilisation
             achieved = pv["valu_g_wave_instr_per_s"] * 64 * pv["lane_utilisation"] / 1e3
-            valu = {"achieved": round(achieved, 3), "frac": round(achieved / VALU_PEAK_TOPS, 4),
-                    "issue_frac": round(pv["valu_g_wave_instr_per_s"] / (N_CU * VALU_WAVE_INSTR_PER_CU_CYCLE *
-                                                                        MAX_CLOCK_GHZ), 4),
+            valu = {"achieved": round(achieved, 3), "frac": round(achieved / peak_tops, 4),
+                    "frac_vs_spec": round(achieved / spec_tops, 4), "spec_peak": round(spec_tops, 2),
+                    "issue_frac": round(pv["valu_g_wave_instr_per_s"] / (N_CU * peak_ipc * MAX_CLOCK_GHZ), 4),
                     "lane_utilisation": pv["lane_utilisation"], "measured_clock_ghz": pv.get("clock_ghz"),
                     "source": f"{os.path.relpath(pmc_valu, ROOT)} ({pv.get('label', '')})"}
-        hbm_rate = traffic / (avg_launch_ms * 1e-3) / 1e9 if traffic else None
+        # PMC bytes per launch (a serialised --pmc run) x launches per frame over the busy time
+        hbm_rate = (traffic * launches_all / world / args.steps / (busy_ms_step * 1e-3) / 1e9
+                    if traffic and busy_ms_step > 0 else None)
         roofline = {
             "bound": "valu",
-            "achieved": valu["achieved"] if valu else None, "peak": round(VALU_PEAK_TOPS, 2),
+            "achieved": valu["achieved"] if valu else None, "peak": round(peak_tops, 2),
             "unit": "T VALU lane-ops/s", "frac": valu["frac"] if valu else None,
             "traffic": traffic, "traffic_unit": "HBM bytes per trace launch (PMC)", "traffic_source": traffic_src,
-            "peak_definition": "256 CUs x 1 wave64 VALU instruction per CU-cycle (measured, profiles/r02_ubench_valu.txt) "
-                               "x 64 lanes x 2.4 GHz; achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation",
+            "peak_definition": f"256 CUs x {peak_ipc:.3f} wave64 VALU instructions per CU-cycle (counter-measured: "
+                               f"{peak_src}) x 64 lanes x 2.4 GHz; valu.frac_vs_spec uses the guide's 2 per CU-cycle; "
+                               "achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation",
             "valu": valu,
             "hbm": {"achieved_gbs": round(hbm_rate, 1) if hbm_rate else None, "peak_gbs": HBM_PEAK_GBS,
-                    "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None},
+                    "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None,
+                    "alg_frac": round(alg_rate_busy / HBM_PEAK_GBS, 4) if alg_rate_busy else None,
+                    "note": "the metric's '% HBM roofline': PMC HBM bytes (frac) and algorithmic bytes (alg_frac) "
+                            "per busy second vs 8 TB/s; the tree and primitives (~0.1 GB) are served from L2 / "
+                            "Infinity Cache, so HBM carries ~5 % of the algorithmic bytes and the kernel is bound "
+                            "by VALU issue instead (frac above)"},
             "l2": {"alg_bytes_per_launch": int(avg_launch_bytes), "alg_bytes_per_ray": round(bytes_per_ray, 1),
                    "model": "64 B per BVH4 node visit + prim_stride B per primitive test",
-                   "achieved_gbs": round(alg_rate, 1), "peak_gbs": L2_PEAK_GBS,
-                   "frac": round(alg_rate / L2_PEAK_GBS, 4)},
+                   "achieved_gbs_per_launch": round(alg_rate, 1),
+                   "achieved_gbs": round(alg_rate_busy, 1) if alg_rate_busy else None, "peak_gbs": L2_PEAK_GBS,
+                   "frac": round(alg_rate_busy / L2_PEAK_GBS, 4) if alg_rate_busy else None},
             **kernel,
         }
     cpu = None

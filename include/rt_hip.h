@@ -186,6 +186,8 @@ typedef struct rt_stats {
   int32_t iterations;  /* logic->trace steps (== trace_kernel launches) */
   int32_t pad;
   uint64_t node_visits; /* count_work only: BVH4 node visits (one 64-B node fetch each) */
+  double trace_busy_ms; /* HIP-event time during which at least one trace_kernel launch ran (the
+                           union of the launches' intervals: slot pipelines overlap theirs) */
 } rt_stats;
 
 typedef struct rt_scene_s* rt_scene_t;

@@ -76,6 +76,7 @@ class rt_stats(ctypes.Structure):
         ("rays", ctypes.c_uint64), ("box_tests", ctypes.c_uint64), ("prim_tests", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
         ("iterations", ctypes.c_int32), ("pad", ctypes.c_int32), ("node_visits", ctypes.c_uint64),
+        ("trace_busy_ms", ctypes.c_double),
     ]
 
 
@@ -212,11 +213,12 @@ class RenderStats:
     trace_ms: float
     iterations: int
     node_visits: int = 0
+    trace_busy_ms: float = 0.0
 
     @staticmethod
     def of(st: rt_stats) -> "RenderStats":
         return RenderStats(int(st.rays), int(st.box_tests), int(st.prim_tests), float(st.kernel_ms),
-                           float(st.trace_ms), int(st.iterations), int(st.node_visits))
+                           float(st.trace_ms), int(st.iterations), int(st.node_visits), float(st.trace_busy_ms))
 
 
 class Scene:

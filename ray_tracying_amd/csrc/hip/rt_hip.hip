@@ -2001,6 +2001,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
         acc.node_visits += st.node_visits;
         acc.kernel_ms += st.kernel_ms;
         acc.trace_ms += st.trace_ms;
+        acc.trace_busy_ms += st.trace_busy_ms;
         acc.iterations += st.iterations;
       }
       if (stats) *stats = acc;
@@ -2189,6 +2190,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
 
   int replay_iter = -1, replay_reps = 0;
   const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
+  const bool steps_log = std::getenv("RT_STEPS_LOG") != nullptr;  // diagnostic: every trace launch, any pipeline
   if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
   if (soft_trace) replay_iter = -1;  // a replay would draw the soft-light samples again from advanced state
   // the diagnostics wait on every step (one pipeline)
@@ -2275,6 +2277,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
 
   // ---- iterate logic -> trace per pipeline until none of its slots issues a query
   double trace_ms = 0.0;
+  std::vector<std::pair<float, float>> busy;  // every trace launch's (start, end) after ev_t0
   int iters = 0;
   unsigned long long diag_prev = 0;
   // steps go out in host batches (one wait per batch, not per step); the first batch is
@@ -2349,8 +2352,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       if (P.done) continue;
       const unsigned int* flag = s->h_flag + (size_t)h * kMaxHostBatch * kFetchStride;
       for (int k = 0; k < batch && !P.done; ++k) {
-        float ms = 0.f;
+        float ms = 0.f, t_a = 0.f, t_b = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[h][k], s->ev_b[h][k]), RT_EDEVICE);
+        if (stats && hipEventElapsedTime(&t_a, s->ev_t0, s->ev_a[h][k]) == hipSuccess &&
+            hipEventElapsedTime(&t_b, s->ev_t0, s->ev_b[h][k]) == hipSuccess)
+          busy.emplace_back(t_a, t_b);
         if (replay_iter == iters && replay_reps > 0 && !p->count_work) {  // one pipeline, batch == 1 here
           // diagnostic (RT_TRACE_REPLAY=iter:reps): re-trace this step's queries; the results
           // are recomputed identically, so the frame is unchanged
@@ -2400,6 +2406,9 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
                        (double)(rc - diag_prev) / (ms * 1e6));
           diag_prev = rc;
         }
+        if (steps_log)
+          std::fprintf(stderr, "[rt steps] pipe %d step %d: any_query %d, trace %.3f ms\n", h, P.steps - batch + k,
+                       (int)more, ms);
         if (more) {  // the final (empty) trace launch -- and any after it in the batch -- is not a traversal step
           trace_ms += ms;
           ++iters;
@@ -2426,6 +2435,19 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     stats->prim_tests = cnt[1];
     stats->kernel_ms = ms;
     stats->trace_ms = trace_ms;
+    std::sort(busy.begin(), busy.end());  // union of the launches' intervals
+    double un = 0.0, cur_a = -1.0, cur_b = -1.0;
+    for (const auto& iv : busy) {
+      if (iv.first > cur_b) {
+        if (cur_b > cur_a) un += cur_b - cur_a;
+        cur_a = iv.first;
+        cur_b = iv.second;
+      } else {
+        cur_b = std::max(cur_b, (double)iv.second);
+      }
+    }
+    if (cur_b > cur_a) un += cur_b - cur_a;
+    stats->trace_busy_ms = un;
     stats->iterations = iters;
 #ifdef RT_PHASE_TIMING
     {

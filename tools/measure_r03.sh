@@ -1,11 +1,12 @@
 #!/bin/bash
 # One GPU measurement pass (run on the GPU box through gpurun):
-#   bash tools/measure_r02.sh LABEL [skip-tests]
-# smoke + GPU parity tests, rocprofv3 kernel-trace stats of the headline bench, PMC passes
-# (FETCH_SIZE, WRITE_SIZE, VALU set; one pass each), the full headline bench (with the CPU
-# baseline) carrying the PMC summaries just measured, then the other BASELINE configs (C2,
-# C3, C4), one rank's share of 2/4/8-way splits, and C5 (4096^2 x 64 spp) on one GPU.
-# Everything lands in gpurun_out/.
+#   bash tools/measure_r03.sh LABEL [skip-tests]
+# smoke + GPU parity tests; rocprofv3 kernel-trace stats of the headline bench; PMC passes
+# (FETCH_SIZE, WRITE_SIZE, the VALU set; one pass each, dispatches serialised by the profiler)
+# and the counter-measured VALU microbenchmark; the full headline bench (with the CPU
+# baseline) carrying the PMC summaries just measured; the other BASELINE configs (C2, C3,
+# C4, C5).  The per-rank shares of split frames: tools/measure_r03_shares.sh.  Everything lands
+# in gpurun_out/.
 set -eo pipefail
 L=${1:?label}
 export TMPDIR=/tmp
@@ -15,7 +16,8 @@ if [ "${2:-}" != "skip-tests" ]; then
   echo "smoke $(date +%T)"
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${L}_smoke.log 2>&1
   echo "gpu tests $(date +%T)"
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${L}_gpu_tests.log 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > gpurun_out/${L}_gpu_tests.log 2>&1
+  tail -1 gpurun_out/${L}_gpu_tests.log
 fi
 echo "kernel trace $(date +%T)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${L}_kt -o kt --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/${L}_kt_bench.json 2> gpurun_out/${L}_kt_bench.err
@@ -23,18 +25,17 @@ echo "pmc $(date +%T)"
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${L}_pmcF -o p --output-format csv -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 > /dev/null 2> gpurun_out/${L}_pmcF.err
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${L}_pmcW -o p --output-format csv -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 > /dev/null 2> gpurun_out/${L}_pmcW.err
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/${L}_pmcV -o p --output-format csv -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 > /dev/null 2> gpurun_out/${L}_pmcV.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/${L}_ubench_pmc -o p --output-format csv -- tools/bin/ubench_valu > gpurun_out/${L}_ubench_src.txt 2>&1
 python3 tools/pmc_traffic.py --fetch gpurun_out/${L}_pmcF --write gpurun_out/${L}_pmcW --kernel "trace_refill_kernel<false" --out gpurun_out/${L}_pmc_traffic.json --label "$L" > /dev/null
 python3 tools/pmc_valu.py --dir gpurun_out/${L}_pmcV --out gpurun_out/${L}_pmc_valu.json --label "$L" > /dev/null
 python3 tools/pmc_valu.py --dir gpurun_out/${L}_pmcV --kernel "logic_kernel" --out gpurun_out/${L}_pmc_valu_logic.json --label "$L" > /dev/null || true
+python3 tools/pmc_ubench.py --dir gpurun_out/${L}_ubench_pmc --out gpurun_out/${L}_ubench_valu_pmc.json --label "$L" > gpurun_out/${L}_ubench_valu_pmc.txt
 echo "bench $(date +%T)"
-timeout -k 10 600 python3 bench.py --steps 10 --warmup 2 --pmc-traffic gpurun_out/${L}_pmc_traffic.json --pmc-valu gpurun_out/${L}_pmc_valu.json > gpurun_out/${L}_bench.json 2> gpurun_out/${L}_bench.err
+timeout -k 10 600 python3 bench.py --steps 10 --warmup 2 --pmc-traffic gpurun_out/${L}_pmc_traffic.json --pmc-valu gpurun_out/${L}_pmc_valu.json --ubench gpurun_out/${L}_ubench_valu_pmc.json > gpurun_out/${L}_bench.json 2> gpurun_out/${L}_bench.err
+cat gpurun_out/${L}_bench.json
 echo "configs $(date +%T)"
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --primary-only --spp-sqrt 1 > gpurun_out/${L}_c2_primary_only_bench.json 2> gpurun_out/${L}_c2.err
 timeout -k 10 300 python3 bench.py --steps 3 --scene $B/Antialiasing.json > gpurun_out/${L}_c3_antialiasing_bench.json 2> gpurun_out/${L}_c3.err
 timeout -k 10 300 python3 bench.py --steps 2 --scene $B/glossy_reflection.json --light-radius 1.0 --light-samples 4 > gpurun_out/${L}_c4_glossy_soft_bench.json 2> gpurun_out/${L}_c4.err
-for N in 2 4 8; do
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --emulate $N --emulate-rank $((N - 1)) > gpurun_out/${L}_emulated_share_of_${N}_bench.json 2> gpurun_out/${L}_em$N.err
-done
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --res 4096 --spp-sqrt 8 > gpurun_out/${L}_c5_4096_64spp_1gpu_bench.json 2> gpurun_out/${L}_c5.err
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --res 4096 --spp-sqrt 8 --emulate 8 --emulate-rank 3 > gpurun_out/${L}_c5_emulated_rank3_of_8_bench.json 2> gpurun_out/${L}_c5e.err
 echo "done $(date +%T)"

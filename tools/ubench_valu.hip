@@ -1,14 +1,17 @@
 // Microbenchmark (diagnostic, not product): VALU issue rate of the instruction kinds the trace
 // kernel's node visit is made of, at 1..8 waves per SIMD, to pin the real VALU peak of gfx950
 // (wave64 instructions per CU-cycle) for the roofline.  Each lane runs 8 independent chains of
-// one instruction kind; the result is wave64 instructions per CU per cycle at the clock
-// measured by s_memtime over the same kernel.
+// one instruction kind.  The printed rate counts the SOURCE-level operations at 2.4 GHz; the
+// authoritative figure is the counter one -- run it under
+//   rocprofv3 --pmc SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- tools/bin/ubench_valu
+// and divide SQ_INSTS_VALU (what the compiler emitted, issued) by 256 CUs x GRBM_GUI_ACTIVE / 8
+// (tools/pmc_ubench.py); dispatches run >= 1 ms so the GRBM clock is accurate.
 // hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize tools/ubench_valu.hip -o tools/bin/ubench_valu
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
 
-constexpr int kIters = 4096;
+constexpr int kIters = 32768;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int KIND>
