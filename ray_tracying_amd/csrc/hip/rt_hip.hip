@@ -1002,6 +1002,9 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
 // scattered state loads, so occupancy pays: without frames 4 waves (<= 128 VGPRs; the
 // unconstrained allocation took 132 = 3 waves, 10 % slower frame); with recursion frames
 // the state machine needs ~195 (2 waves).  A/B builds: make variant VDEFS=-DRT_LOGIC_WAVES=5
+#ifndef RT_LOGIC_HIT_AFTER_RES
+#define RT_LOGIC_HIT_AFTER_RES 1  // A/B: 0 loads a closest query's hit record before its result is known
+#endif
 #ifndef RT_LOGIC_WAVES
 #define RT_LOGIC_WAVES 4
 #endif
@@ -1078,9 +1081,9 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
         mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
         store_hit_pnm(hit_rec(a.hit, slot), hp, hn, (uint32_t)mat_id);
         if (kTex) a.hit_uv[slot] = make_float2(hu, hv);
-      } else if (st0 == ST_SHADOW || st0 == ST_CLOSEST) {
+      } else if (st0 == ST_SHADOW || (st0 == ST_CLOSEST && (!RT_LOGIC_HIT_AFTER_RES || res_ld >= 0))) {
         // the hit being shaded: its record (written by the trace kernel for planes-only scenes,
-        // by the ST_CLOSEST step above otherwise)
+        // by the ST_CLOSEST step above otherwise); a closest miss does not read it
         const HitRec hr = load_hit(hit_rec(a.hit, slot));
         hp = hr.p;
         hn = hr.n;
