@@ -45,13 +45,13 @@ namespace {
 
 constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
 constexpr int kBlock = 256;
-// default LDS stack entries per lane (RT_LDS_STACK overrides): 16 for the traversal instances
-// that continue shadow chains (5 waves/SIMD), 12 for the plain one, which runs 6 waves/SIMD
-// (6 blocks x 24 KB of LDS per CU)
-constexpr int kLdsStack = 16, kLdsStackPlain = 12;
-static int lds_stack_entries(bool plain) {  // read per call: tests vary it within one process
+// default LDS stack entries per lane (RT_LDS_STACK overrides): 12 for the traversal instances
+// that run 6 waves/SIMD (6 blocks x 24 KB of LDS per CU), 16 for the one at 5 (fused
+// point-light shadows over transformed shapes: its hit-record code needs the registers)
+constexpr int kLdsStack = 16, kLdsStack6 = 12;
+static int lds_stack_entries(bool six_waves) {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_LDS_STACK");
-  return e ? std::max(1, std::min(64, std::atoi(e))) : plain ? kLdsStackPlain : kLdsStack;
+  return e ? std::max(1, std::min(64, std::atoi(e))) : six_waves ? kLdsStack6 : kLdsStack;
 }
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
@@ -658,10 +658,12 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
                           // 5 fits without spills once the SLP vectoriser is off (Makefile)
 #endif
 #ifndef RT_TRACE_WAVES_PLAIN
-#define RT_TRACE_WAVES_PLAIN 6  // the plain instance (no shadow chains): 6 waves/SIMD, 80 VGPRs
-#endif
+#define RT_TRACE_WAVES_PLAIN 6  // every other instance: 6 waves/SIMD, 80 VGPRs (r03: plain headline
+#endif                          // +1.7 %, C5 +1.1 %; fused planes / soft shadows +1-2 %)
+// waves per SIMD of an instance: 5 only for fused shadows over transformed shapes (C3 -1..-3 % at 6)
+#define RT_INSTANCE_WAVES(kPlanesOnly, kFuse) ((kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : RT_TRACE_WAVES_PLAIN)
 template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu((kFuse || kSoft) ? RT_TRACE_WAVES : RT_TRACE_WAVES_PLAIN, 8))) void trace_refill_kernel(TraceArgs ta) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse), 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_work;
   const int lane = threadIdx.x & 63;
@@ -1689,7 +1691,7 @@ struct rt_scene_s {
   void* d_prim_refs = nullptr;
   void* d_ref_boxes = nullptr;
   int n_cu = 0, trace_blocks_per_cu = 0;  // plain traversal instance
-  int trace_blocks_per_cu_chain = 0;        // instances that continue shadow chains (kFuse / kSoft)
+  int trace_blocks_per_cu_fuse = 0, trace_blocks_per_cu_soft = 0;  // shadow-chain instances (kFuse / kSoft)
   bool late_draws = false;  // a light with radius > 0 or a rough material: draws after a sample's start
   bool soft_lights = false;  // a light with radius > 0 (several shadow samples with -light_sample > 1)
   int* d_spill = nullptr;
@@ -1940,8 +1942,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const bool planes = d->prim_stride == 64;
-    auto occupancy = [&](const void* fn, bool plain) {
-      const int lds_entries = std::min(d->stack_bound, lds_stack_entries(plain));
+    auto occupancy = [&](const void* fn, bool six_waves) {
+      const int lds_entries = std::min(d->stack_bound, lds_stack_entries(six_waves));
       const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
       int b = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, lds_bytes) != hipSuccess || b < 1) b = 2;
@@ -1950,8 +1952,10 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     };
     bpc = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, false>
                            : (const void*)trace_refill_kernel<false, false, false, false>, true);
-    s->trace_blocks_per_cu_chain = occupancy(planes ? (const void*)trace_refill_kernel<false, true, true, false>
-                                                    : (const void*)trace_refill_kernel<false, false, true, false>, false);
+    s->trace_blocks_per_cu_fuse = occupancy(planes ? (const void*)trace_refill_kernel<false, true, true, false>
+                                                   : (const void*)trace_refill_kernel<false, false, true, false>, planes);
+    s->trace_blocks_per_cu_soft = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, true>
+                                                   : (const void*)trace_refill_kernel<false, false, false, true>, true);
     s->n_cu = ncu;
     s->trace_blocks_per_cu = bpc;
   }
@@ -2197,9 +2201,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // RT_FUSE=0 / 1 overrides (1: whenever the scene allows it).
   ta.n_fuse = n_units <= 2LL * n_slots || s->desc.n_prims < kFuseFewPrims ? s->fuse_lights : 0;
   if (const char* e = std::getenv("RT_FUSE")) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
-  // the launched instance: plain (6 waves/SIMD, 12 LDS stack entries) or a shadow-chain one
-  const bool plain_launch = ta.n_fuse == 0 && !soft_trace;
-  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(plain_launch));
+  // the launched instance (launch_trace2): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
+  // entries except fused shadows over transformed shapes (5, 16)
+  const bool fuse_launch = ta.n_fuse > 0, soft_launch = !fuse_launch && soft_trace;
+  const bool six_waves = !(fuse_launch && !planes_only);
+  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(six_waves));
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
   la.occl = s->d_occl;
@@ -2241,8 +2247,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   } pipes[kPipes];
   const int per_pipe = (n_slots / kBlock / n_pipes) * kBlock;
   const int spill_entries = std::max(0, s->desc.stack_bound - ta.lds_entries);
-  const unsigned grid_cap =
-      (unsigned)std::max(1, s->n_cu * (plain_launch ? s->trace_blocks_per_cu : s->trace_blocks_per_cu_chain));
+  const unsigned grid_cap = (unsigned)std::max(
+      1, s->n_cu * (fuse_launch ? s->trace_blocks_per_cu_fuse : soft_launch ? s->trace_blocks_per_cu_soft : s->trace_blocks_per_cu));
   size_t spill_need = 0;
   for (int h = 0; h < n_pipes; ++h) {
     Pipe& P = pipes[h];
