@@ -254,6 +254,8 @@ struct TraceArgs {
   int soft_start;
   int frames, pinhole;
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
+  int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
+  float* help_hit;            // [n_threads][HIT_STRIDE]: a drain helper's closest-hit record
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
 #endif
@@ -307,7 +309,7 @@ __device__ __forceinline__ bool plane_leaf_fast_ok(const PrimA& P, const Ray& r,
 // normal, shapes.cpp:472-480, and the material) to the slot's hit record when it is found --
 // a closer hit overwrites it -- so the write-back needs no re-test and no register holds it
 // across the traversal.
-template <bool kCount, bool kPlanesOnly>
+template <bool kCount, bool kPlanesOnly, bool kDrain = false>
 __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int first, int cnt, const Ray& r, bool any,
                                            float tmax, uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
   for (int k = 0; k < cnt; ++k) {
@@ -342,8 +344,10 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
       h.best_t = t;
       h.best_ref = ref.x;
       h.best_idx = pi;
-      if (kPlanesOnly && !a.has_tex) {
-        store_hit_pnm(hit_rec(a.hit, slot), X, V3{P.a[3], P.a[7], P.a[11]}, RT_TAG_MATERIAL(prim_tag(P)));
+      if (kPlanesOnly && !a.has_tex) {  // a drain helper (no slot of its own): its lane's record
+        float* R = !kDrain || slot >= 0 ? hit_rec(a.hit, slot)
+                                        : a.help_hit + (size_t)(blockIdx.x * kBlock + threadIdx.x) * HIT_STRIDE;
+        store_hit_pnm(R, X, V3{P.a[3], P.a[7], P.a[11]}, RT_TAG_MATERIAL(prim_tag(P)));
       }
     }
   }
@@ -510,6 +514,19 @@ __device__ __forceinline__ int stack_pop_live(const TraceArgs& a, const LaneStac
     if (!(__int_as_float(v.y) > lim)) return v.x;
   }
   return kNoItem;
+}
+
+// Drain: removes and returns the lane's bottom stack entry -- pushed first, so the farthest
+// pending subtree of the query -- and moves the others down one, so sp never exceeds the
+// serial traversal's depth bound (the order of the rest is kept).
+__device__ __forceinline__ int2 stack_take_bottom(const TraceArgs& a, const LaneStack& S, int& sp, int gtid) {
+  auto at = [&](int i) -> int2* {
+    return i < a.lds_entries ? S.e + i * kBlock : S.spill + (size_t)(i - a.lds_entries) * a.n_threads + gtid;
+  };
+  const int2 b = *at(0);
+  for (int i = 1; i < sp; ++i) *at(i - 1) = *at(i);
+  --sp;
+  return b;
 }
 
 __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, const HitState& h) {
@@ -883,7 +900,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       RT_PT_MARK(0);  // refill: write-back, work fetch, query setup
       // done when the queue is drained and every lane settled (a query with nothing to
       // traverse -- linear mode, empty scene -- is settled in the next refill phase)
-      if (exhausted && __ballot(slot >= 0) == 0ull) break;
+      // (drain_help: the queries still traversing go on in the drain loop below)
+      if (exhausted && (a.drain_help || __ballot(slot >= 0) == 0ull)) break;
     }
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
     const uint64_t leafm = __ballot(is_leaf_item(item));
@@ -906,6 +924,128 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
 #else
     if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
 #endif
+  }
+  // ---- drain (drain_help: the queue is dry).  A query still traversing keeps its lane (its
+  // owner); a free lane becomes a helper: it takes the bottom entry of a busy lane's stack --
+  // pushed first, the farthest subtree pending there -- and searches it with the owner's ray
+  // under the owner's bound, re-read every iteration.  A finished helper's best hit is folded
+  // into its owner's (lower t, then lower reference index: the minimum the serial traversal
+  // finds in any visiting order; any-hit: occluded), and an owner settles only once no helper
+  // searches for it, so every result is the serial traversal's.  A soup ray that crosses the
+  // scene without a hit visits hundreds of nodes; without help it alone holds its wave (and
+  // the launch) long after the queue ran dry.
+  if (a.drain_help) {
+    int own = -1;  // helper: lane of the owner whose query it searches
+    int nh = 0;    // owner: helpers searching for its query
+    for (;;) {
+      // fold finished helpers into their owners
+      uint64_t fin = __ballot(own >= 0 && item == kNoItem);
+      if (fin != 0ull) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // helpers' records
+      while (fin != 0ull) {
+        const int hl = __ffsll((long long)fin) - 1;
+        fin &= fin - 1ull;
+        const int o = __builtin_amdgcn_readlane(own, hl);
+        const float bt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h.best_t), hl));
+        const int br = __builtin_amdgcn_readlane(h.best_ref, hl);
+        const int bi = __builtin_amdgcn_readlane(h.best_idx, hl);
+        const int bd = __builtin_amdgcn_readlane((int)h.done, hl);
+        if (lane == o) {
+          --nh;
+          if (q.any) {
+            if (bd) {
+              h.done = true;
+              item = kNoItem;
+            }
+          } else if (bi >= 0 && (bt < h.best_t || (bt == h.best_t && br < h.best_ref))) {
+            h.best_t = bt;
+            h.best_ref = br;
+            h.best_idx = bi;
+            lim = cull_limit(a, q, h);
+            if (kPlanesOnly && !a.has_tex) {  // the helper's record becomes the slot's
+              const float4* src = reinterpret_cast<const float4*>(a.help_hit + (size_t)(gtid - lane + hl) * HIT_STRIDE);
+              float4* dst = reinterpret_cast<float4*>(hit_rec(a.hit, slot));
+              const float4 w0 = src[0], w1 = src[1];
+              dst[0] = w0;
+              dst[1] = w1;
+            }
+          }
+        }
+      }
+      if (own >= 0 && item == kNoItem) {
+        own = -1;
+        sp = 0;
+      }
+      // an owner whose traversal and helpers are done settles (and may start its next query)
+      if (slot >= 0 && item == kNoItem && nh == 0) settle();
+      if (__ballot(slot >= 0) == 0ull) break;
+      // pair free lanes with lanes that have stack entries (k-th free lane, k-th donor)
+      const bool can_give = item != kNoItem && sp > 0;
+      const uint64_t D = __ballot(can_give), I = __ballot(slot < 0 && own < 0);
+      if (D != 0ull && I != 0ull) {
+        const int k = min(__popcll(D), __popcll(I));
+        const int rootv = own >= 0 ? own : lane;
+        int src = -1;
+        uint64_t d = D, fr = I;
+        for (int j = 0; j < k; ++j) {
+          const int dl = __ffsll((long long)d) - 1, il = __ffsll((long long)fr) - 1;
+          d &= d - 1ull;
+          fr &= fr - 1ull;
+          if (lane == il) src = dl;
+          if (lane == __builtin_amdgcn_readlane(rootv, dl)) ++nh;
+        }
+        int2 ent = make_int2(kNoItem, 0);
+        if (can_give && __popcll(D & lane_lt) < k) ent = stack_take_bottom(a, S, sp, gtid);
+        const int s2 = src >= 0 ? src : lane;
+        const int ge = __shfl(ent.x, s2), gt = __shfl(ent.y, s2), rs = __shfl(rootv, s2);
+        const int qs = src >= 0 ? rs : lane;  // receivers copy their owner's query
+        q.r.o.x = __shfl(q.r.o.x, qs);
+        q.r.o.y = __shfl(q.r.o.y, qs);
+        q.r.o.z = __shfl(q.r.o.z, qs);
+        q.r.d.x = __shfl(q.r.d.x, qs);
+        q.r.d.y = __shfl(q.r.d.y, qs);
+        q.r.d.z = __shfl(q.r.d.z, qs);
+        q.r.time = __shfl(q.r.time, qs);
+        q.inv.x = __shfl(q.inv.x, qs);
+        q.inv.y = __shfl(q.inv.y, qs);
+        q.inv.z = __shfl(q.inv.z, qs);
+        q.tmax = __shfl(q.tmax, qs);
+        q.any = __shfl((int)q.any, qs) != 0;
+        q.par = (uint32_t)__shfl((int)q.par, qs);
+        q.sel[0] = (uint32_t)__shfl((int)q.sel[0], qs);
+        q.sel[1] = (uint32_t)__shfl((int)q.sel[1], qs);
+        q.sel[2] = (uint32_t)__shfl((int)q.sel[2], qs);
+        const float rl = __shfl(lim, qs);
+        if (src >= 0) {
+          own = rs;
+          h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
+          lim = rl;
+          sp = 0;
+          item = __int_as_float(gt) > rl ? kNoItem : ge;
+        }
+      }
+      // helpers take their owner's bound (closest: its best so far; any-hit: occluded ends it)
+      if (__ballot(own >= 0) != 0ull) {
+        const int os = own >= 0 ? own : lane;
+        const float ol = __shfl(lim, os);
+        const int od = __shfl((int)h.done, os);
+        if (own >= 0) {
+          if (od) item = kNoItem;
+          else if (ol < lim) lim = ol;
+        }
+      }
+      const uint64_t act = __ballot(item != kNoItem);
+      const uint64_t leafm = __ballot(is_leaf_item(item));
+      if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+        if (is_leaf_item(item)) {
+          const uint32_t e = (uint32_t)item;
+          test_prims<kCount, kPlanesOnly, true>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax,
+                                                q.par, true, h, nprim);
+          lim = cull_limit(a, q, h);
+          item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
+        }
+      }
+      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+    }
   }
   RT_PT_FLUSH
 #ifdef RT_EXIT_TIMING
@@ -2183,6 +2323,9 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.refill_min = refill_min_env();
   ta.leaf_min = leaf_min_env();
   ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
+  // free lanes help the queries still traversing once a launch's queue is dry (RT_DRAIN_HELP=0 off)
+  ta.drain_help = 1;
+  if (const char* e = std::getenv("RT_DRAIN_HELP")) ta.drain_help = std::atoi(e) != 0 ? 1 : 0;
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
   for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
@@ -2247,6 +2390,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   } pipes[kPipes];
   const int per_pipe = (n_slots / kBlock / n_pipes) * kBlock;
   const int spill_entries = std::max(0, s->desc.stack_bound - ta.lds_entries);
+  constexpr int kHelpHitEntries = HIT_STRIDE * 4 / 8;  // a helper's hit record, in spill entries (8 B)
   const unsigned grid_cap = (unsigned)std::max(
       1, s->n_cu * (fuse_launch ? s->trace_blocks_per_cu_fuse : soft_launch ? s->trace_blocks_per_cu_soft : s->trace_blocks_per_cu));
   size_t spill_need = 0;
@@ -2266,7 +2410,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     P.logic_blocks = (unsigned)(count / kBlock);
     P.trace_blocks = std::min(grid_cap, (unsigned)((count + kBlock - 1) / kBlock));
     P.ta.n_threads = (int)P.trace_blocks * kBlock;
-    spill_need += (size_t)spill_entries * P.ta.n_threads;
+    spill_need += (size_t)(spill_entries + kHelpHitEntries) * P.ta.n_threads;
     P.iters = 0;
     P.steps = 0;
     P.done = false;
@@ -2281,6 +2425,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   for (int h = 0, off = 0; h < n_pipes; ++h) {  // each pipeline's traversal spills into its own range
     pipes[h].ta.spill = s->d_spill + (size_t)2 * off;
     off += spill_entries * pipes[h].ta.n_threads;
+    pipes[h].ta.help_hit = reinterpret_cast<float*>(s->d_spill + (size_t)2 * off);  // drain helpers' records after it
+    off += kHelpHitEntries * pipes[h].ta.n_threads;
   }
 #ifdef RT_EXIT_TIMING
   static unsigned long long* exit_log = nullptr;

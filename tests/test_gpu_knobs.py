@@ -8,7 +8,8 @@ slots split into two pipelines on two streams, soft-shadow samples advanced by
 shadow_step_kernel or by the logic kernel instead of the tracing lane, the greedy BVH4
 collapse instead of the SAH-optimal one, point-light shadow rays left unfused in a small
 call, one or four slot pipelines instead of the default two, and the tiles rendered in the
-caller's order instead of costliest first (small calls' default).
+caller's order instead of costliest first (small calls' default), and the lanes still
+traversing when a launch's queue runs dry left alone instead of helped by the free lanes.
 """
 import os
 import subprocess
@@ -51,6 +52,8 @@ KNOBS = [
     {"RT_PIPES": "1"},  # one slot pipeline (the default is two on two streams)
     {"RT_TILE_ORDER": "0"},  # tiles in the caller's order (small calls render costliest tiles first)
     {"RT_PIPES": "4", "RT_SLOTS": "8192"},  # four pipelines of two slot blocks each
+    {"RT_DRAIN_HELP": "0"},  # no drain helpers: each query traversed by its own lane alone
+    {"RT_DRAIN_HELP": "1", "RT_LDS_STACK": "2", "RT_LEAF_MIN": "1"},  # helpers take entries from the HBM spill area
 ]
 
 
