@@ -1752,7 +1752,7 @@ void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, unsig
 }
 static int pipes_env() {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_PIPES");
-  return e ? std::max(1, std::min(kPipes, std::atoi(e))) : 2;
+  return e ? std::max(1, std::min(kPipes, std::atoi(e))) : 1;
 }
 
 static int fetch_shards_env() {
@@ -2182,17 +2182,14 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const long long n_units = (long long)n_pixels * n_samples;
   if (n_units > 0x7ffffff0LL) return fail(RT_EINVAL, "rt_render_tiles: too many samples in one call (split the tiles)");
   // whole blocks of slots; a wave renders 64 consecutive samples per batch
-  // Slots in flight (r03 sweep, two pipelines, one box; Mrays/s): every sample of a call of at
-  // most 32M units (one rank's quarter of the headline frame, 26M: 4913 at 16M slots -> 5211 all
-  // in flight); larger calls 0.45 of their units, between 32M and 96M (headline 105M units:
-  // 16M 5554, 40M 5756, 48M 5835, 52M 5458 -- at half the frame each pipeline's steps fall into
-  // lockstep and the drains coincide; C5 1.07G units: 16M 6630, 48M 7157, 96M 7290; C3 16M
-  // 19547, 52M 20348); scenes with reflection / refraction keep 16M (C4 16M 13680, 52M 13023:
-  // their slots carry the Trace frames and take many short steps).
+  // Slots in flight (r03 sweep with one pipeline and drain helpers, one box; Mrays/s): every
+  // sample of a call of at most 128M units -- the whole headline frame (105M: 32M 6167, 48M
+  // 6263, 64M 6184, all 6319) or one rank's half of it (52M: 32M 5885, all 6225) -- else 128M
+  // (C5 1.07G units: 96M 7666, 128M 7703, 192M 7705); scenes with reflection / refraction keep
+  // 16M (C4: 8M 13043, 16M 13065, 32M 12791: their slots carry the Trace frames and take many
+  // short steps).  ~180 B of HBM per slot: 128M slots ~23 GB.
   const bool frames_scene = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
-  long long slots = n_units <= (32LL << 20) ? n_units
-                    : frames_scene          ? (16LL << 20)
-                                            : std::max(32LL << 20, std::min(96LL << 20, n_units * 45 / 100));
+  long long slots = frames_scene ? std::min(n_units, 16LL << 20) : std::min(n_units, 128LL << 20);
   if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
   const int n_slots = (int)(((std::min<long long>(n_units, slots) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {  // render-order tile ids, then their output positions
@@ -2368,14 +2365,14 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const bool step_sync = diag || replay_iter >= 0;
 #endif
 
-  // ---- pipelines: the slots split into independent logic -> trace sequences, one per stream
-  // (units are claimed from the shared batch counters, so the split changes no value): one
-  // pipeline's trace launch drains (its last waves finish their last rays) and its logic and
-  // start steps run while the other pipeline's traversal fills the machine.  Measured (r03,
-  // one box, RT_PIPES=1/2/3/4): headline 4967/5521/5337/5181 Mrays/s, C5 5869/6551/6428/6331,
-  // one rank's eighth 4306/4467/4282/4306, C3 19082/19769/18702/19094, C4 12656/13037/13461/
-  // 13518; a call of one launch (C2, 1 spp primary only: 1M units) 1462/1193 -- two pipelines
-  // by default, one for calls of at most 4M units (a second pipeline only adds a launch tail).
+  // ---- pipelines: the slots may split into independent logic -> trace sequences, one per
+  // stream (units are claimed from the shared batch counters, so the split changes no value):
+  // one pipeline's trace launch drains and its logic and start steps run while the other
+  // pipeline's traversal fills the machine.  Before the drain helpers two pipelines won
+  // (headline 4967 vs 5521 Mrays/s); with them the drain is short and one pipeline wins
+  // everywhere (r03, one box, RT_PIPES=2 vs 1): headline 6050 / 6251, one rank's half / quarter /
+  // eighth 5535 / 5875, 5239 / 5948, 4961 / 5357, C3 19955 / 20374, C4 12782 / 12979, C5 7492 /
+  // 7683 -- one by default, RT_PIPES=2..4 on request.
   int n_pipes = n_units <= (4LL << 20) ? 1 : pipes_env();
   if (const char* e = std::getenv("RT_PIPES")) n_pipes = pipes_env();  // an explicit request holds for any size
   if (step_sync) n_pipes = 1;
@@ -2391,8 +2388,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const int per_pipe = (n_slots / kBlock / n_pipes) * kBlock;
   const int spill_entries = std::max(0, s->desc.stack_bound - ta.lds_entries);
   constexpr int kHelpHitEntries = HIT_STRIDE * 4 / 8;  // a helper's hit record, in spill entries (8 B)
-  const unsigned grid_cap = (unsigned)std::max(
-      1, s->n_cu * (fuse_launch ? s->trace_blocks_per_cu_fuse : soft_launch ? s->trace_blocks_per_cu_soft : s->trace_blocks_per_cu));
+  // a call of at most 4M units runs one short launch: one block per CU fewer shortens each
+  // ray's latency and so the launch's tail (C2, 1M units: 6 / 5 / 4 blocks 1679 / 1772 / 1790
+  // Mrays/s; one rank's eighth, 13M units: 5 and 6 within 1 %)
+  const int call_bpc = fuse_launch ? s->trace_blocks_per_cu_fuse : soft_launch ? s->trace_blocks_per_cu_soft : s->trace_blocks_per_cu;
+  const unsigned grid_cap = (unsigned)std::max(1, s->n_cu * (n_units <= (4LL << 20) ? std::max(1, call_bpc - 1) : call_bpc));
   size_t spill_need = 0;
   for (int h = 0; h < n_pipes; ++h) {
     Pipe& P = pipes[h];
