@@ -62,7 +62,7 @@ def valu_peak(path):
             return float(d["max_valu_wave_instr_per_cu_cycle"]), f"{os.path.relpath(path, ROOT)} ({d.get('label', '')})"
     return 1.0, "assumed 1 wave64 instruction per CU-cycle (no counter-measured microbenchmark found)"
 NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
-PMC_PROFILE = "r03_v6"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r03_v7"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
