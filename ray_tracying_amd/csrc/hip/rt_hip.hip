@@ -163,6 +163,24 @@ struct Common {
   float eps_abs;
 };
 
+// Division by a call-invariant divisor (n / d for any 32-bit n; n % d from it): one mul_hi and
+// three ALU ops instead of the ~20-instruction expansion of an integer division.  m =
+// floor(2^32 (2^l - d) / d) + 1 with l = ceil(log2 d); q = (t + ((n - t) >> min(l, 1))) >> max(l - 1, 0)
+// where t = mul_hi(n, m) (Granlund-Montgomery round-up method).
+struct FastDiv {
+  uint32_t m, s1, s2;
+};
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& d) {
+  const uint32_t t = __umulhi(n, d.m);
+  return (t + ((n - t) >> d.s1)) >> d.s2;
+}
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, l < 1 ? l : 1u, l > 1 ? l - 1 : 0u};
+}
+
 struct LogicArgs {
   Common c;
   const rt_material* mats;
@@ -179,6 +197,7 @@ struct LogicArgs {
   int tile_affine;            // tile_ids[i] == tile_first + i * tile_step (no table lookup)
   int tile_first, tile_step;
   int tile_w, tile_h, tiles_x, sub_x;
+  FastDiv fd_tile_px, fd_sub_x, fd_tiles_x, fd_samples;  // the divisions of pixel_coords / unit_coords
   int n_pixels;  // n_tiles * tile_w * tile_h (launch-local pixel space)
   int n_samples; // s*s (1 when s <= 1)
   long long n_units;  // n_pixels * n_samples
@@ -1114,12 +1133,14 @@ __device__ __forceinline__ Ray camera_ray(const rt_camera_desc& c, float px, flo
 // consecutive slots trace spatially coherent rays.
 __device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, int& y, size_t& out_off) {
   const int tile_px = a.tile_w * a.tile_h;
-  const int tl = p / tile_px, r = p - tl * tile_px;
+  const int tl = (int)fdiv((uint32_t)p, a.fd_tile_px), r = p - tl * tile_px;
   const int b = r >> 6, l = r & 63;
-  const int lx = (b % a.sub_x) * 8 + (l & 7), ly = (b / a.sub_x) * 8 + (l >> 3);
+  const int by = (int)fdiv((uint32_t)b, a.fd_sub_x), bx = b - by * a.sub_x;
+  const int lx = bx * 8 + (l & 7), ly = by * 8 + (l >> 3);
   const int tid = a.tile_affine ? a.tile_first + tl * a.tile_step : a.tile_ids[tl];
-  x = (tid % a.tiles_x) * a.tile_w + lx;
-  y = (tid / a.tiles_x) * a.tile_h + ly;
+  const int ty = (int)fdiv((uint32_t)tid, a.fd_tiles_x), tx = tid - ty * a.tiles_x;
+  x = tx * a.tile_w + lx;
+  y = ty * a.tile_h + ly;
   const int to = a.tile_out ? a.tile_out[tl] : tl;
   out_off = ((size_t)to * tile_px + (size_t)ly * a.tile_w + lx) * 3;
   return x < a.cam.res_x && y < a.cam.res_y;
@@ -1130,7 +1151,7 @@ __device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, 
 __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, int& px, int& py, int& sample) {
   // units < 2^31 (checked on the host): 32-bit unsigned division
   const unsigned u = (unsigned)unit, ns = (unsigned)a.n_samples;
-  const int p = (int)(u / ns);
+  const int p = (int)fdiv(u, a.fd_samples);
   sample = (int)(u - (unsigned)p * ns);
   size_t off;
   return pixel_coords(a, p, px, py, off);
@@ -1160,6 +1181,11 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
   const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
   // a wave whose slots all retired has nothing left in this frame (one scalar load)
   if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
+  // no batch left for this wave's shard: a wave whose slots all finish now retires at the end
+  // of this step (below), so its finished slots need no idle marks
+  const int wave = slot >> 6, shard = wave % a.batch_shards;
+  const unsigned claimed = __hip_atomic_load(a.batch_ctr + shard * kCtrStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool no_batch = ((long long)claimed * a.batch_shards + shard) * 64 >= a.n_units;
   bool want = false;
   if (slot < a.slot_end) {
     const int N = a.n_slots;
@@ -1477,11 +1503,14 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
           }
         }
       }
+      const bool wave_wants_here = __ballot(want) != 0ull;  // lanes outside this block want nothing
       if (fast || st0 < 0) {
         // advanced by shadow_step_kernel / idle since an earlier step: nothing changes
       } else if (!want) {  // the sample finished: idle until the wave's batch is done
-        stu(F_UNIT, (uint32_t)-2);
-        store_no_query(a.query, N, slot);
+        if (!no_batch || wave_wants_here) {  // (a wave that retires now is never read again)
+          stu(F_UNIT, (uint32_t)-2);
+          store_no_query(a.query, N, slot);
+        }
       } else {
         stu(F_CTRL, (uint32_t)st | ((uint32_t)depth << 4));
         if (a.late_draws) stu(F_RNG, rng.ctr);
@@ -1505,11 +1534,16 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
   }
   // tell the host another step is needed: a plain store, no atomic (all writers store 1); a
   // slot-wave left with no query (every sample of its batch finished) is flagged for
-  // start_kernel, which pulls its next batch in this same step
+  // start_kernel, which pulls its next batch in this same step -- or retired here when its
+  // shard's claim counter is already past the call's units (start_kernel's claim could only
+  // retire it: a call whose samples were all in flight skips that pass over every slot)
   const bool wave_wants = __ballot(want) != 0ull;
   if ((threadIdx.x & 63) == 0) {
-    if (wave_wants) *a.any_query = 1u;
-    else a.wave_done[slot >> 6] = kWaveIdle;
+    if (wave_wants) {
+      *a.any_query = 1u;
+    } else {
+      a.wave_done[wave] = no_batch ? 1u : kWaveIdle;
+    }
   }
 }
 
@@ -2272,8 +2306,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.tile_h = tile_h;
   la.tiles_x = tiles_x;
   la.sub_x = tile_w / 8;
+  la.fd_tile_px = make_fastdiv((uint32_t)(tile_w * tile_h));
+  la.fd_sub_x = make_fastdiv((uint32_t)la.sub_x);
+  la.fd_tiles_x = make_fastdiv((uint32_t)tiles_x);
   la.n_pixels = n_pixels;
   la.n_samples = n_samples;
+  la.fd_samples = make_fastdiv((uint32_t)n_samples);
   la.n_units = n_units;
   la.samples = s->d_samples;
   la.out = d_out;
