@@ -8,7 +8,8 @@ soup (planes with c3 == c0, splitmix64 seed 20251226), 1024x1024, -s 10 (100 jit
 refraction + shadow rays), counted by the kernels.  One step = one full frame.
 
 N GPUs: one process per GPU (torch.distributed, RCCL); the frame's 64x64 tiles are dealt
-to the ranks on a 2-D lattice (tiles.tile_rank; image-tile data parallelism, fixed total work -> "strong"
+to the ranks in equal counts balanced by a projected-centre cost estimate (tiles.balanced_deal;
+--deal lattice: the 2-D lattice; image-tile data parallelism, fixed total work -> "strong"
 scaling), each rank renders its tiles into a device buffer and rank 0 gathers the packed
 tiles over RCCL/xGMI inside the timed step.  value = all ranks' rays / max-over-ranks time.
 
@@ -133,6 +134,8 @@ def parse():
     ap.add_argument("--emulate", type=int, default=0,
                     help="diagnostic: render only rank --emulate-rank's tiles of an N-way split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--deal", choices=["balanced", "lattice"], default="balanced",
+                    help="tiles -> ranks: equal counts balanced by the projected-centre cost estimate, or the 2-D lattice")
     ap.add_argument("--light-radius", type=float, default=None,
                     help="override every light's radius (SURVEY.md 8(d) C4: soft shadows, e.g. 1.0)")
     ap.add_argument("--primary-only", action="store_true",
@@ -279,10 +282,15 @@ def main():
     T = args.tile
     tiles_x, tiles_y = tl.tile_grid(W, H, T)
     n_tiles = tiles_x * tiles_y
-    mine = tl.assign_tiles(n_tiles, world, rank, tiles_x)
+    # tiles -> ranks: equal tile counts, balanced by the projected-centre cost estimate (every
+    # rank computes the same deal from the same scene); --deal lattice: the 2-D lattice
+    split = world if world > 1 else (args.emulate if args.emulate > 1 else 1)
+    deal = tl.balanced_deal(ds.tile_costs(T, T), split) if split > 1 and args.deal == "balanced" else None
+    mine = tl.assign_tiles(n_tiles, world, rank, tiles_x, deal)
     if args.emulate > 1 and world == 1:  # one rank's share of an N-way split (scaling prediction)
-        mine = tl.assign_tiles(n_tiles, args.emulate, args.emulate_rank, tiles_x)
-    out = torch.zeros(tl.tiles_per_rank(n_tiles, world, tiles_x) * T * T * 3, dtype=torch.float32, device=f"cuda:{dev}")
+        mine = tl.assign_tiles(n_tiles, args.emulate, args.emulate_rank, tiles_x, deal)
+    out = torch.zeros(tl.tiles_per_rank(n_tiles, world, tiles_x, deal) * T * T * 3, dtype=torch.float32,
+                      device=f"cuda:{dev}")
     gathered = None
     log(f"[rank {rank}] scene {W}x{H}, {scene.info.n_shapes} shapes, {scene.info.n_nodes} nodes, depth "
         f"{scene.info.tree_depth}, load+build {load_s:.1f} s; {len(mine)} tiles on cuda:{dev}")
@@ -341,14 +349,14 @@ def main():
     elapsed = tmax.item()
 
     if rank == 0 and dist:  # sanity: the gathered frame has every pixel, all finite
-        img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H)
+        img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H, deal)
         assert np.isfinite(img).all()
     if args.dump_frame:  # one more frame at the first timed seed, gathered, saved by rank 0
         step(args.seed)
         torch.cuda.synchronize()
         if rank == 0:
             parts = [g.cpu().numpy() for g in gathered] if dist else [out.cpu().numpy()]
-            np.save(args.dump_frame, tl.unpack(parts, world, n_tiles, T, W, H))
+            np.save(args.dump_frame, tl.unpack(parts, world, n_tiles, T, W, H, deal))
 
     if rank != 0:
         if dist:
@@ -453,7 +461,7 @@ def main():
         "config": {
             "workload": workload,
             "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample {args.light_samples}",
-            "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}",
+            "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}" + (f" ({args.deal} deal)" if split > 1 else ""),
             "rng": "counter (splitmix64 per pixel/sample)",
             **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),
         },

@@ -211,6 +211,15 @@ int rt_render_tiles(rt_scene_t scene, const rt_camera_desc* cam, const rt_render
                     const int32_t* tile_ids, int32_t n_tiles, int32_t tile_w, int32_t tile_h,
                     float* d_rgb_out, void* stream, rt_stats* stats);
 
+/* Per-tile cost estimate of a frame (host only, no device work): for every tile of the
+ * ceil(res_x/tile_w) x ceil(res_y/tile_h) grid (tile id order), how many of a sample of up to
+ * 64K primitive centres project into it through `cam` -- the estimate rt_render_tiles orders
+ * single-step calls by.  costs_out holds one float per tile.  Multi-GPU callers deal tiles to
+ * ranks by it (ray_tracying_amd/tiles.py balanced_deal); every rank computes the same values
+ * from the same scene.  No reference counterpart: the reference renders serially
+ * (Code/raytracer.cpp:433-476). */
+int rt_tile_costs(rt_scene_t scene, const rt_camera_desc* cam, int32_t tile_w, int32_t tile_h, float* costs_out);
+
 /* Small device-memory helpers so non-torch callers (ctypes tests, the C++ CLI) can drive
  * rt_render_tiles without their own HIP runtime bindings. */
 int rt_malloc(int32_t device, size_t bytes, void** d_ptr);

@@ -99,7 +99,7 @@ _host = None
 HIP_SYMBOLS = [
     "rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_tiles", "rt_malloc",
     "rt_free", "rt_memcpy_d2h", "rt_memcpy_h2d", "rt_synchronize", "rt_build_info", "rt_last_error",
-    "rt_quantise_device",
+    "rt_quantise_device", "rt_tile_costs",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_free", "rth_scene_get_info", "rth_scene_desc", "rth_scene_camera",
@@ -138,6 +138,7 @@ def _load():
     _hip.rt_memcpy_d2h.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     _hip.rt_memcpy_h2d.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     _hip.rt_quantise_device.argtypes = [c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p]
+    _hip.rt_tile_costs.argtypes = [c.c_void_p, c.POINTER(rt_camera_desc), c.c_int32, c.c_int32, c.POINTER(c.c_float)]
     _hip.rt_synchronize.argtypes = [c.c_int32]
     _host.rth_last_error.restype = c.c_char_p
     _host.rth_scene_load.argtypes = [c.c_char_p, c.c_char_p, c.c_int32, c.c_int32, c.POINTER(c.c_void_p)]
@@ -306,6 +307,16 @@ class DeviceScene:
                                         ctypes.c_void_p(int(stream) if stream else 0), ctypes.byref(st)),
                    "rt_render_tiles")
         return RenderStats.of(st)
+
+
+    def tile_costs(self, tile_w: int, tile_h: int) -> np.ndarray:
+        """rt_tile_costs: per-tile cost estimate (projected primitive centres), tile id order."""
+        tx = (self.cam.res_x + tile_w - 1) // tile_w
+        ty = (self.cam.res_y + tile_h - 1) // tile_h
+        out = np.zeros(tx * ty, dtype=np.float32)
+        _check_hip(_hip.rt_tile_costs(self._h, ctypes.byref(self.cam), int(tile_w), int(tile_h),
+                                      out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), "rt_tile_costs")
+        return out
 
 
 def unpack_tiles(packed: np.ndarray, tile_ids, tile_w: int, tile_h: int, width: int, height: int) -> np.ndarray:

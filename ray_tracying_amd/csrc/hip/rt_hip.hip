@@ -1924,12 +1924,10 @@ static void free_workspace(rt_scene_s* s) {
 // background tiles come last, in every launch and at the end of the call.  Scheduling only:
 // every sample is keyed by its pixel (counter RNG), so the order changes no value.  The
 // per-tile costs are cached per camera and tile size.
-static void tile_cost_order(rt_scene_s* s, const rt_camera_desc* cam, int tile_w, int tile_h, int tiles_x, int tiles_y,
-                            const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
-  order.resize((size_t)n_tiles);
-  for (int i = 0; i < n_tiles; ++i) order[i] = i;
-  if (const char* e = std::getenv("RT_TILE_ORDER")) wanted = std::atoi(e) != 0;  // 0 / 1: never / always
-  if (!wanted || n_tiles < 2 || s->cost_pts.empty()) return;
+// Per-tile cost estimate for `cam` and the tile size (cached on the scene): how many of the
+// sampled primitive centres project into each tile of the grid.
+static const std::vector<float>& tile_costs(rt_scene_s* s, const rt_camera_desc* cam, int tile_w, int tile_h, int tiles_x,
+                                            int tiles_y) {
   std::vector<unsigned char> key(sizeof(rt_camera_desc) + 2 * sizeof(int));
   std::memcpy(key.data(), cam, sizeof(rt_camera_desc));
   std::memcpy(key.data() + sizeof(rt_camera_desc), &tile_w, sizeof(int));
@@ -1951,8 +1949,18 @@ static void tile_cost_order(rt_scene_s* s, const rt_camera_desc* cam, int tile_w
       s->tile_cost[(size_t)((int)py / tile_h) * tiles_x + (int)px / tile_w] += 1.0f;
     }
   }
+  return s->tile_cost;
+}
+
+static void tile_cost_order(rt_scene_s* s, const rt_camera_desc* cam, int tile_w, int tile_h, int tiles_x, int tiles_y,
+                            const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
+  order.resize((size_t)n_tiles);
+  for (int i = 0; i < n_tiles; ++i) order[i] = i;
+  if (const char* e = std::getenv("RT_TILE_ORDER")) wanted = std::atoi(e) != 0;  // 0 / 1: never / always
+  if (!wanted || n_tiles < 2 || s->cost_pts.empty()) return;
+  const std::vector<float>& cost = tile_costs(s, cam, tile_w, tile_h, tiles_x, tiles_y);
   std::stable_sort(order.begin(), order.end(), [&](int i, int j) {
-    return s->tile_cost[(size_t)tile_ids[i]] > s->tile_cost[(size_t)tile_ids[j]];
+    return cost[(size_t)tile_ids[i]] > cost[(size_t)tile_ids[j]];
   });
 }
 
@@ -2158,6 +2166,16 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   s->desc.ref_leaf_boxes = nullptr;
   s->desc.lights = nullptr; s->desc.textures = nullptr; s->desc.texels = nullptr;
   *out = s;
+  return RT_OK;
+}
+
+int rt_tile_costs(rt_scene_t s, const rt_camera_desc* cam, int32_t tile_w, int32_t tile_h, float* costs_out) {
+  if (!s || !cam || !costs_out) return fail(RT_EINVAL, "rt_tile_costs: null argument");
+  if (tile_w <= 0 || tile_h <= 0) return fail(RT_EINVAL, "rt_tile_costs: tile size must be positive");
+  if (cam->res_x <= 0 || cam->res_y <= 0) return fail(RT_EINVAL, "rt_tile_costs: camera resolution is 0");
+  const int tiles_x = (cam->res_x + tile_w - 1) / tile_w, tiles_y = (cam->res_y + tile_h - 1) / tile_h;
+  const std::vector<float>& cost = tile_costs(s, cam, tile_w, tile_h, tiles_x, tiles_y);
+  std::memcpy(costs_out, cost.data(), cost.size() * sizeof(float));
   return RT_OK;
 }
 
