@@ -8,9 +8,9 @@ soup (planes with c3 == c0, splitmix64 seed 20251226), 1024x1024, -s 10 (100 jit
 refraction + shadow rays), counted by the kernels.  One step = one full frame.
 
 N GPUs: one process per GPU (torch.distributed, RCCL); the frame's 64x64 tiles are dealt
-to the ranks in equal counts balanced by a projected-centre cost estimate (tiles.balanced_deal;
---deal lattice: the 2-D lattice; image-tile data parallelism, fixed total work -> "strong"
-scaling), each rank renders its tiles into a device buffer and rank 0 gathers the packed
+to the ranks on a 2-D lattice (tiles.tile_rank; --deal balanced: equal counts balanced by a
+projected-centre cost estimate, measured slower; image-tile data parallelism, fixed total
+work -> "strong" scaling), each rank renders its tiles into a device buffer and rank 0 gathers the packed
 tiles over RCCL/xGMI inside the timed step.  value = all ranks' rays / max-over-ranks time.
 
 roofline: the traversal kernel (trace_refill_kernel) is bound by
@@ -63,7 +63,7 @@ def valu_peak(path):
             return float(d["max_valu_wave_instr_per_cu_cycle"]), f"{os.path.relpath(path, ROOT)} ({d.get('label', '')})"
     return 1.0, "assumed 1 wave64 instruction per CU-cycle (no counter-measured microbenchmark found)"
 NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
-PMC_PROFILE = "r03_v7"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r03_v8"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
@@ -134,7 +134,7 @@ def parse():
     ap.add_argument("--emulate", type=int, default=0,
                     help="diagnostic: render only rank --emulate-rank's tiles of an N-way split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0)
-    ap.add_argument("--deal", choices=["balanced", "lattice"], default="balanced",
+    ap.add_argument("--deal", choices=["balanced", "lattice"], default="lattice",
                     help="tiles -> ranks: equal counts balanced by the projected-centre cost estimate, or the 2-D lattice")
     ap.add_argument("--light-radius", type=float, default=None,
                     help="override every light's radius (SURVEY.md 8(d) C4: soft shadows, e.g. 1.0)")
@@ -282,8 +282,9 @@ def main():
     T = args.tile
     tiles_x, tiles_y = tl.tile_grid(W, H, T)
     n_tiles = tiles_x * tiles_y
-    # tiles -> ranks: equal tile counts, balanced by the projected-centre cost estimate (every
-    # rank computes the same deal from the same scene); --deal lattice: the 2-D lattice
+    # tiles -> ranks: the 2-D lattice; --deal balanced: equal tile counts balanced by the
+    # projected-centre cost estimate (every rank computes the same deal from the same scene;
+    # its slowest rank measured slower than the lattice's)
     split = world if world > 1 else (args.emulate if args.emulate > 1 else 1)
     deal = tl.balanced_deal(ds.tile_costs(T, T), split) if split > 1 and args.deal == "balanced" else None
     mine = tl.assign_tiles(n_tiles, world, rank, tiles_x, deal)

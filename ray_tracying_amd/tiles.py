@@ -43,7 +43,9 @@ def balanced_deal(costs, world: int) -> np.ndarray:
     processing time first under a count cap).  Equal tile counts keep the per-sample passes
     (camera rays, shading, reduce) equal; the greedy evens out the traversal.  The 1M-triangle
     headline frame split 8 ways: the lattice's busiest rank holds 1.027x the mean of projected
-    centres, this deal 1.0001x.  Deterministic: every rank computes the same deal."""
+    centres, this deal 1.0001x -- yet its slowest rank measured slower than the lattice's (the
+    estimate misses the cost of rays grazing the object), so it is not bench.py's default.
+    Deterministic: every rank computes the same deal."""
     costs = np.asarray(costs, dtype=np.float64).ravel()
     n = costs.size
     cap = np.array([n // world + (1 if r < n % world else 0) for r in range(world)])
