@@ -56,6 +56,14 @@ asan: $(LIB)/librt_hip.so $(LIB)/librt_comm.so
 	cp $(LIB)/librt_hip.so $(LIB)/librt_comm.so ray_tracying_amd/lib_asan/
 	$(MAKE) -C oracle asan SANFLAGS="$(SANFLAGS)"
 
+# The counter-measured VALU peak (tools/measure_r03.sh runs it under rocprofv3 --pmc): built
+# with the device code's own flags -- with the SLP vectoriser on, the mixed int / convert /
+# fp32 kind becomes v_pk_add_f32 + moves and issues at 1.18 instead of 1.73 per CU-cycle
+ubench: tools/bin/ubench_valu
+tools/bin/ubench_valu: tools/ubench_valu.hip
+	@mkdir -p tools/bin
+	$(HIPCC) $(filter-out -fPIC,$(HIPFLAGS)) tools/ubench_valu.hip -o $@
+
 oracle:
 	$(MAKE) -C oracle all
 
@@ -66,4 +74,4 @@ clean:
 	rm -rf $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle ref clean variant asan
+.PHONY: all oracle ref clean variant asan ubench

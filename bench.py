@@ -52,7 +52,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 #     4 SIMDs per CU = 2 instructions per CU-cycle (78.6 T lane-ops/s)
 N_CU, MAX_CLOCK_GHZ = 256, 2.4
 SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE = 2.0
-UBENCH_PROFILE = "r03_v6"  # committed counter-measured VALU microbenchmark (profiles/)
+UBENCH_PROFILE = "r03_v9"  # committed counter-measured VALU microbenchmark (profiles/)
 
 
 def valu_peak(path):
