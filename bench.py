@@ -7,7 +7,9 @@ soup (planes with c3 == c0, splitmix64 seed 20251226), 1024x1024, -s 10 (100 jit
 -bvh, -light_sample 1.  A ray is one BVH::get_intersection call (camera + reflection +
 refraction + shadow rays), counted by the kernels.  One step = one full frame.
 
-N GPUs: one process per GPU (torch.distributed, RCCL); the frame's 64x64 tiles are dealt
+N GPUs: one process per GPU (torch.distributed, RCCL).  `bench.py --gpus N` started directly
+spawns the N ranks itself (a child torch.distributed.run, before any GPU call); under an
+external launcher WORLD_SIZE must equal --gpus.  The frame's 64x64 tiles are dealt
 to the ranks on a 2-D lattice (tiles.tile_rank; --deal balanced: equal counts balanced by a
 projected-centre cost estimate, measured slower; image-tile data parallelism, fixed total
 work -> "strong" scaling), each rank renders its tiles into a device buffer and rank 0 gathers the packed
@@ -17,16 +19,18 @@ roofline: the traversal kernel (trace_refill_kernel) is bo
 VALU issue, not by bytes -- the tree and primitives (~0.1 GB) stay on-die -- so the line
 reports it against the VALU peak: useful lane-operations per second (wave64 VALU
 instructions x 64 x lane utilisation, from the committed rocprofv3 PMC pass of the same
-build) over 256 CUs x 1 wave64 instruction per CU-cycle (measured: tools/ubench_valu.hip)
-x 2.4 GHz.  Beside it, per average trace launch (HIP
+build) over 256 CUs x the highest wave64 VALU issue rate per CU-cycle that SQ_INSTS_VALU
+shows for tools/ubench_valu.hip's instruction streams (1.73, a mixed int / convert / fp32
+stream; the guide's spec 2 per CU-cycle beside it) x 2.4 GHz.  Beside it, per average trace launch (HIP
 events on the launch stream over the timed steps): `hbm` = PMC HBM bytes (traffic) / launch
 time vs 8 TB/s, and `l2` = algorithmic bytes (64 B per BVH4 node visit + 64 B per primitive
 test, counted by an instrumented run of the same frame) / launch time vs the L2's 34.5 TB/s.
 Scenes of a few primitives (C1-C4) get no roofline claim.
 cpu_baseline: the compiled reference (oracle/_ref/ref_driver; kind "reference") -- or the
 oracle restatement if the reference binary is absent (kind "port") -- on rank 0 at N=1,
-single-threaded, on a bounded row band of the same frame; plus the same band size run as
-16 concurrent single-threaded processes (the job's CPU share on the GPU box).
+single-threaded, on a bounded sample of the same frame (12 rows spread evenly over it; its
+rays/sample beside the frame's); plus the same number of rows run as 16 concurrent
+single-threaded processes (the job's CPU share on the GPU box).
 """
 from __future__ import annotations
 
@@ -117,9 +121,50 @@ def host_cpus() -> dict:
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+def launch_plan(gpus, env) -> tuple[str, object]:
+    """How this invocation runs, decided before anything touches the GPU:
+    ("run", world)    -- render as one rank of `world` (WORLD_SIZE from torchrun, or 1);
+    ("spawn", n)      -- --gpus n > 1 without WORLD_SIZE: start n ranks as a child
+                         torch.distributed.run (one process per GPU), relay its exit code;
+    ("error", msg)    -- --gpus disagrees with the WORLD_SIZE an external launcher set."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        n = 1 if gpus is None else int(gpus)
+        if n < 1:
+            return "error", f"bench.py: --gpus {n} must be >= 1"
+        return ("spawn", n) if n > 1 else ("run", 1)
+    world = int(ws)
+    if gpus is not None and int(gpus) != world:
+        return "error", (f"bench.py: --gpus {gpus} but WORLD_SIZE={world} (set by the launcher); "
+                         "pass the same rank count to both, or drop the launcher and let --gpus spawn the ranks")
+    return "run", world
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus n` run directly: the ranks are a child `torch.distributed.run` (this
+    process imports neither torch nor HIP, so nothing is exec'd after GPU init).  Every rank
+    inherits stdout, so rank 0's JSON line is the run's output; a failed rank fails the run."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log(f"bench.py: spawning {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); > 1 without WORLD_SIZE spawns them (torch.distributed.run), "
+                         "with WORLD_SIZE set it must equal it; default: WORLD_SIZE, else 1")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="diagnostic: set up the ranks and their process group, print the rank count, render nothing")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--tris", type=int, default=1_000_000)
@@ -158,27 +203,39 @@ def parse():
     return ap.parse_args()
 
 
-def _cpu_cmd(scene_path: str, args, y0: int, y1: int):
+def _cpu_cmd(scene_path: str, args, y0: int, y1: int, step: int = 1):
     W = args.res
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
     if os.path.exists(ref):
         return [ref, "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt), "-light_sample", str(args.light_samples),
-                "-seed", "42", "-rows", str(y0), str(y1)], "reference"
+                "-seed", "42", "-rows", str(y0), str(y1), "-row-step", str(step)], "reference"
+    # the oracle restatement renders one contiguous band (its -region)
     return [os.path.join(ROOT, "oracle", "oracle_cli"), "-input", scene_path, "-bvh", "-s", str(args.spp_sqrt),
             "-light_sample", str(args.light_samples), "-rng", "counter", "-seed", str(args.seed), "-region", "0",
             str(y0), str(W),
             str(y1 - y0)], "port"
 
 
-def cpu_baseline(scene_path: str, args, rank: int):
-    """Reference CPU path on a bounded sample: a centred band of rows of the same frame, on
-    one core; then the same band size on each of N cores at once, as N
-    concurrent single-threaded processes on disjoint bands (the reference cannot split one
-    image across threads)."""
+def cpu_baseline(scene_path: str, args, rank: int, frame_rays_per_sample: float | None = None):
+    """Reference CPU path on a bounded sample of the same frame: --cpu-rows rows spread evenly
+    over it (every k-th row, k = H // rows, starting at k // 2: the soup's dense centre and its
+    background in proportion), on one core; then the same number of rows on
+    each of N cores at once, as N concurrent single-threaded processes on disjoint row sets
+    (offset within the stride; the reference cannot split one image across threads)."""
     W = H = args.res
-    y0 = H // 2 - args.cpu_rows // 2
-    y1 = y0 + args.cpu_rows
-    cmd, kind = _cpu_cmd(scene_path, args, y0, y1)
+    n_rows = max(1, min(args.cpu_rows, H))
+    k = max(1, H // n_rows)
+    spp = max(1, args.spp_sqrt) ** 2
+
+    def rows_for(off):  # rows off, off + k, ... : n_rows of them
+        return off, min(H, off + (n_rows - 1) * k + 1)
+
+    y0, y1 = rows_for(k // 2)
+    cmd, kind = _cpu_cmd(scene_path, args, y0, y1, k)
+    if kind == "port":  # contiguous centre band
+        y0 = H // 2 - n_rows // 2
+        y1 = y0 + n_rows
+        cmd, kind = _cpu_cmd(scene_path, args, y0, y1)
     if not os.path.exists(cmd[0]):
         return None
     t0 = time.time()
@@ -190,26 +247,34 @@ def cpu_baseline(scene_path: str, args, rank: int):
     st = json.loads(r.stdout.strip().splitlines()[-1])
     rays = st["rays"]
     secs = st["render_seconds"]
+    rows_desc = (f"{n_rows} rows spread over the {W}x{H} frame (rows {y0}, {y0 + k}, ... {y1 - 1}: every {k}th)"
+                 if kind == "reference" else f"rows {y0}-{y1 - 1} of the {W}x{H} frame")
+    rps = rays / (W * n_rows * spp)
     out = {
         "value": rays / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": kind,
-        "sample": (f"rows {y0}-{y1 - 1} of the {W}x{H} frame at {args.spp_sqrt ** 2} spp "
-                   f"({W * (y1 - y0)} px, {rays} rays, render {secs:.1f} s single-threaded; "
-                   f"scene load + BVH build {st['load_seconds']:.1f} s excluded; wall {wall:.1f} s)"),
+        "sample": (f"{rows_desc} at {spp} spp ({W * n_rows} px, {rays} rays = {rps:.3f} rays/sample"
+                   + (f" vs the whole frame's {frame_rays_per_sample:.3f}" if frame_rays_per_sample else "")
+                   + f"; render {secs:.1f} s single-threaded; scene load + BVH build {st['load_seconds']:.1f} s "
+                   f"excluded; wall {wall:.1f} s)"),
+        "sample_rays_per_sample": round(rps, 4),
+        "frame_rays_per_sample": round(frame_rays_per_sample, 4) if frame_rays_per_sample else None,
     }
     n = args.cpu_procs
     if n > 1:
-        # disjoint bands of the same height, packed around the centre of the frame
-        band = args.cpu_rows
-        first = max(0, H // 2 - (n * band) // 2)
         jobs = []
-        for k in range(n):
-            a0 = min(H - band, first + k * band)
-            c, _ = _cpu_cmd(scene_path, args, a0, a0 + band)
+        for j in range(n):
+            if kind == "reference":  # disjoint row sets: offsets spread within the stride
+                a0, a1 = rows_for((k // 2 + j * max(1, k // n)) % k)
+                c, _ = _cpu_cmd(scene_path, args, a0, a1, k)
+            else:  # disjoint bands packed around the centre
+                first = max(0, H // 2 - (n * n_rows) // 2)
+                a0 = min(H - n_rows, first + j * n_rows)
+                c, _ = _cpu_cmd(scene_path, args, a0, a0 + n_rows)
             jobs.append(subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd="/tmp"))
         rates, total = [], 0
-        for j in jobs:
-            so, se = j.communicate()
-            if j.returncode != 0:
+        for jb in jobs:
+            so, se = jb.communicate()
+            if jb.returncode != 0:
                 log("cpu baseline (all cores) failed:", se[-1000:])
                 return out
             stk = json.loads(so.strip().splitlines()[-1])
@@ -219,23 +284,42 @@ def cpu_baseline(scene_path: str, args, rank: int):
         out["procs"] = n
         out["host_cpus"] = host_cpus()
         out["sample_multi_proc"] = (f"{n} concurrent single-threaded processes (one per usable core, at most 16), "
-                                    f"{band} rows each ({total} rays); value = sum of the per-process rates")
+                                    f"{n_rows} rows each ({total} rays); value = sum of the per-process rates")
     return out
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    how, what = launch_plan(args.gpus, os.environ)
+    if how == "error":
+        log(what)
+        sys.exit(2)
+    if how == "spawn":
+        sys.exit(spawn_ranks(what))
+    world = what
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    import ray_tracying_amd as rt
-    from ray_tracying_amd import tiles as tl
 
     # RT_BENCH_BACKEND=gloo: rehearsal of the N-rank path with more ranks than GPUs (ranks
     # share devices, collectives through host memory) -- functional checks only, not a metric
     backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
     dist = None
+    if args.dry_run:  # launcher check without a GPU: process group, one collective, the rank count
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            t = torch.tensor([1.0])
+            dist.all_reduce(t)
+            world = int(t.item())
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_in_group": world}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
+    import ray_tracying_amd as rt
+    from ray_tracying_amd import tiles as tl
+
     dev = local_rank if backend == "nccl" else local_rank % max(torch.cuda.device_count(), 1)
     coll = f"cuda:{dev}" if backend == "nccl" else "cpu"
     if world > 1:
@@ -444,7 +528,7 @@ def main():
         }
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(scene_path, args, rank)
+        cpu = cpu_baseline(scene_path, args, rank, rays_all / args.steps / (W * H * max(1, args.spp_sqrt) ** 2))
     line = {
         "metric": METRIC,
         "value": round(value, 3),

@@ -184,11 +184,16 @@ typedef struct rt_stats {
   double kernel_ms;    /* HIP-event time of the whole render (all logic+trace steps) */
   double trace_ms;     /* HIP-event time summed over the trace_kernel launches only */
   int32_t iterations;  /* logic->trace steps (== trace_kernel launches) */
-  int32_t pad;
+  int32_t path;        /* RT_PATH_ONE_PASS when every chunk of the call ran one-pass (camera rays,
+                          one trace launch, shading + reduction), RT_PATH_STEPS for the step
+                          pipeline (logic -> trace steps over slot state) */
   uint64_t node_visits; /* count_work only: BVH4 node visits (one 64-B node fetch each) */
   double trace_busy_ms; /* HIP-event time during which at least one trace_kernel launch ran (the
                            union of the launches' intervals: slot pipelines overlap theirs) */
 } rt_stats;
+
+#define RT_PATH_STEPS 0
+#define RT_PATH_ONE_PASS 1
 
 typedef struct rt_scene_s* rt_scene_t;
 

@@ -9,7 +9,10 @@
 // and AABB tests by wrapping AABB::intersect (shapes.cpp:55) -- no reference source edits.
 //
 // usage: ref_driver -input scene.json [-bvh] [-s N] [-light_sample N] [-seed S]
-//                   [-float-out file.f32] [-ppm-out file.ppm] [-rows y0 y1]
+//                   [-float-out file.f32] [-ppm-out file.ppm] [-rows y0 y1] [-row-step k]
+// -row-step k renders only rows y0, y0 + k, ... < y1 (a sample spread over the frame, for the
+// CPU baseline; the float output then holds those rows in order)
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -51,7 +54,7 @@ bool __wrap__ZNK4AABB9intersectERK3Ray(const AABB* self, const Ray& r) {
 int main(int argc, char** argv) {
   std::string input, fout, pout;
   bool use_bvh = false;
-  int s = 4, ls = 1, y0 = -1, y1 = -1;
+  int s = 4, ls = 1, y0 = -1, y1 = -1, step = 1;
   unsigned long long seed = 1;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "-bvh")) use_bvh = true;
@@ -62,6 +65,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "-float-out") && i + 1 < argc) fout = argv[++i];
     else if (!strcmp(argv[i], "-ppm-out") && i + 1 < argc) pout = argv[++i];
     else if (!strcmp(argv[i], "-rows") && i + 2 < argc) { y0 = atoi(argv[++i]); y1 = atoi(argv[++i]); }
+    else if (!strcmp(argv[i], "-row-step") && i + 1 < argc) step = std::max(1, atoi(argv[++i]));
   }
   if (input.empty()) { std::cerr << "ref_driver: -input required\n"; return 2; }
   auto t0 = std::chrono::steady_clock::now();
@@ -78,12 +82,13 @@ int main(int argc, char** argv) {
   if (y0 < 0) { y0 = 0; y1 = height; }
   auto t1 = std::chrono::steady_clock::now();
   unsigned long long boxes_before = g_boxes;
-  std::vector<float> fb((size_t)width * (y1 - y0) * 3);
+  const int n_rows = (y1 - y0 + step - 1) / step;
+  std::vector<float> fb((size_t)width * n_rows * 3);
   Image img(width, height);
-  for (int y = y0; y < y1; ++y) {
+  for (int y = y0; y < y1; y += step) {
     for (int x = 0; x < width; ++x) {
       Color c = compute_pixel_color(x, y, s, camera, bvh, lights, use_bvh, gen, dist, ls);
-      size_t i = ((size_t)(y - y0) * width + x) * 3;
+      size_t i = ((size_t)((y - y0) / step) * width + x) * 3;
       fb[i] = c.r; fb[i + 1] = c.g; fb[i + 2] = c.b;
       float gamma = 1.1f;  // raytracer.cpp:446-457
       float r = std::pow(c.r, 1.0f / gamma), g = std::pow(c.g, 1.0f / gamma), b = std::pow(c.b, 1.0f / gamma);
@@ -99,8 +104,8 @@ int main(int argc, char** argv) {
   }
   if (!pout.empty()) img.write(pout);
   double ld = std::chrono::duration<double>(t1 - t0).count(), rd = std::chrono::duration<double>(t2 - t1).count();
-  printf("{\"width\": %d, \"height\": %d, \"rows\": [%d, %d], \"rays\": %llu, \"box_tests\": %llu, "
-         "\"load_seconds\": %.6f, \"render_seconds\": %.6f, \"n_shapes\": %zu, \"n_lights\": %zu}\n",
-         width, height, y0, y1, g_rays, g_boxes - boxes_before, ld, rd, shapes.size(), lights.size());
+  printf("{\"width\": %d, \"height\": %d, \"rows\": [%d, %d], \"row_step\": %d, \"n_rows\": %d, \"rays\": %llu, "
+         "\"box_tests\": %llu, \"load_seconds\": %.6f, \"render_seconds\": %.6f, \"n_shapes\": %zu, \"n_lights\": %zu}\n",
+         width, height, y0, y1, step, n_rows, g_rays, g_boxes - boxes_before, ld, rd, shapes.size(), lights.size());
   return 0;
 }

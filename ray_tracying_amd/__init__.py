@@ -75,7 +75,7 @@ class rt_stats(ctypes.Structure):
     _fields_ = [
         ("rays", ctypes.c_uint64), ("box_tests", ctypes.c_uint64), ("prim_tests", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double), ("trace_ms", ctypes.c_double),
-        ("iterations", ctypes.c_int32), ("pad", ctypes.c_int32), ("node_visits", ctypes.c_uint64),
+        ("iterations", ctypes.c_int32), ("path", ctypes.c_int32), ("node_visits", ctypes.c_uint64),
         ("trace_busy_ms", ctypes.c_double),
     ]
 
@@ -205,6 +205,9 @@ class RenderParams:
                                 1 if self.count_work else 0, int(self.seed) & (2**64 - 1), 1, 0)
 
 
+PATH_STEPS, PATH_ONE_PASS = 0, 1  # rt_stats.path (include/rt_hip.h)
+
+
 @dataclass
 class RenderStats:
     rays: int
@@ -215,11 +218,13 @@ class RenderStats:
     iterations: int
     node_visits: int = 0
     trace_busy_ms: float = 0.0
+    path: int = 0  # PATH_ONE_PASS: camera rays, one trace launch, shading + reduction; PATH_STEPS: the step pipeline
 
     @staticmethod
     def of(st: rt_stats) -> "RenderStats":
         return RenderStats(int(st.rays), int(st.box_tests), int(st.prim_tests), float(st.kernel_ms),
-                           float(st.trace_ms), int(st.iterations), int(st.node_visits), float(st.trace_busy_ms))
+                           float(st.trace_ms), int(st.iterations), int(st.node_visits), float(st.trace_busy_ms),
+                           int(st.path))
 
 
 class Scene:
@@ -311,7 +316,9 @@ class DeviceScene:
 
     def tile_costs(self, tile_w: int, tile_h: int) -> np.ndarray:
         """rt_tile_costs: per-tile cost estimate (projected primitive centres), tile id order."""
-        tx = (self.cam.res_x + tile_w - 1) // tile_w
+        if int(tile_w) <= 0 or int(tile_h) <= 0:
+            raise NativeError(f"rt_tile_costs: tile size must be positive (got {tile_w}x{tile_h})")
+        tx =(self.cam.res_x + tile_w - 1) // tile_w
         ty = (self.cam.res_y + tile_h - 1) // tile_h
         out = np.zeros(tx * ty, dtype=np.float32)
         _check_hip(_hip.rt_tile_costs(self._h, ctypes.byref(self.cam), int(tile_w), int(tile_h),

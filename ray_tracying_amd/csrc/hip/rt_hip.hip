@@ -103,6 +103,7 @@ struct HitRec {
 };
 __device__ __forceinline__ float* hit_rec(float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
 __device__ __forceinline__ const float* hit_rec(const float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
+__device__ __forceinline__ const float* hit_rec_u(const float* hit, size_t unit) { return hit + unit * HIT_STRIDE; }
 // point + normal + material
 __device__ __forceinline__ void store_hit_pnm(float* R, V3 p, V3 n, uint32_t mat) {
   *reinterpret_cast<float4*>(R) = make_float4(p.x, p.y, p.z, n.x);
@@ -230,6 +231,9 @@ struct LogicArgs {
   const unsigned int* occl;
   unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it);
                             // kWaveIdle from logic_kernel to start_kernel: every slot is idle
+  // one-pass calls (camera_kernel -> one trace launch -> shade_reduce_kernel; slot == unit)
+  int op_kind;           // some tile reaches past the image: the query's kind word marks those units
+  int op_time;           // scenes with transformed shapes: the camera ray's time is stored (moving spheres)
 };
 
 struct TraceArgs {
@@ -274,6 +278,8 @@ struct TraceArgs {
   int frames, pinhole;
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
+  int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
+  int op_kind, op_time;       // one-pass: read the kind word (units outside the image) / the ray time
   float* help_hit;            // [n_threads][HIT_STRIDE]: a drain helper's closest-hit record
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
@@ -419,6 +425,15 @@ __device__ __forceinline__ void setup_query(Query& q, V3 o, V3 d, float tq, bool
 
 // Reads slot's query record; false if the slot emitted no query this step.
 __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query& q) {
+  if (a.one_pass) {  // the unit's camera ray (camera_kernel): 64-bit field offsets (up to 2^30 slots)
+    const size_t n = (size_t)(unsigned)a.n_slots, u = (size_t)(unsigned)slot;
+    if (a.op_kind && __float_as_int(a.query[Q_KIND * n + u]) < 0) return false;
+    const V3 o = a.pinhole ? V3{a.cam_loc[0], a.cam_loc[1], a.cam_loc[2]}
+                           : V3{a.query[(Q_O + 0) * n + u], a.query[(Q_O + 1) * n + u], a.query[(Q_O + 2) * n + u]};
+    setup_query(q, o, V3{a.query[(Q_D + 0) * n + u], a.query[(Q_D + 1) * n + u], a.query[(Q_D + 2) * n + u]},
+                a.op_time ? a.query[Q_TMAX * n + u] : 0.0f, false);
+    return true;
+  }
   const int N = a.n_slots;
   const int kind = __float_as_int(a.query[Q_KIND * N + slot]);
   if (kind < 0) return false;
@@ -856,8 +871,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           soft_first();
           return;
         }
-        fz = 1;
-        next = 0;
+        if (a.n_fuse > 0) {  // (a one-pass call without lights launches this instance for the record alone)
+          fz = 1;
+          next = 0;
+        }
       }
     }
     if (kFuse && next >= 0) fused_shadow(next);
@@ -889,7 +906,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
               q_next = (unsigned)ta.slot_base + g * 64u;
               q_end = (unsigned)ta.slot_base + min(g * 64u + 64u, nq);
               // 64-slot groups are slot-waves of the logic step: skip one whose slots retired
-              if (a.wave_done[q_next >> 6] != 0u) continue;
+              if (!a.one_pass && a.wave_done[q_next >> 6] != 0u) continue;
               break;
             }
             if (++sk >= (int)nfs) {
@@ -1547,6 +1564,60 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
   }
 }
 
+// compute_pixel_color (raytracer.cpp:18-70): the camera ray of sample `sample` of pixel (px,
+// py) -- its RNG stream, the stratified jitter in double, Camera::pixelToRay_thin_lens (the
+// lens draws for an aperture > 0).  The ray's time is the caller's next draw.
+__device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, int sample, Rng& rng) {
+  rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
+  const int s = a.spp_sqrt;
+  float fx, fy;
+  if (s <= 1) {
+    fx = (float)px + 0.5f;
+    fy = (float)py + 0.5f;
+  } else {
+    int si = sample % s, sj = sample / s;
+    double ox = rng.next();
+    double oy = rng.next();
+    double sx = ((double)si + ox) / (double)s;
+    double sy = ((double)sj + oy) / (double)s;
+    fx = (float)((double)px + sx);
+    fy = (float)((double)py + sy);
+  }
+  return camera_ray(a.cam, fx, fy, rng);
+}
+
+// One-pass calls (every sample of the call traced by one launch; no Trace recursion, point
+// lights only, so no draw after a sample's start): each unit's camera ray -- start_kernel's
+// ops -- written to the query record of the slot with the unit's own index, and nothing else:
+// the direction; the origin for a thin-lens camera; the ray time for scenes with transformed
+// shapes (moving spheres; a plane ignores it, so planes-only scenes skip that draw); a kind
+// word only when some tile reaches past the image (those units: -1, and a miss result).
+__global__ __launch_bounds__(kBlock) void camera_kernel(LogicArgs a) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.any_query = 1u;  // the trace launch runs
+  const long long unit = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (unit >= a.n_units) return;
+  const size_t N = (size_t)(unsigned)a.n_slots, u = (size_t)unit;
+  float* Q = a.query;
+  int px, py, sample;
+  if (!unit_coords(a, unit, px, py, sample)) {  // edge tile: pixel outside the image
+    Q[Q_KIND * N + u] = __int_as_float(-1);
+    a.result[u] = -1;
+    return;
+  }
+  Rng rng;
+  const Ray ray = sample_ray(a, px, py, sample, rng);
+  Q[(Q_D + 0) * N + u] = ray.d.x;
+  Q[(Q_D + 1) * N + u] = ray.d.y;
+  Q[(Q_D + 2) * N + u] = ray.d.z;
+  if (!a.pinhole) {
+    Q[(Q_O + 0) * N + u] = ray.o.x;
+    Q[(Q_O + 1) * N + u] = ray.o.y;
+    Q[(Q_O + 2) * N + u] = ray.o.z;
+  }
+  if (a.op_time) Q[Q_TMAX * N + u] = (float)rng.next();
+  if (a.op_kind) Q[Q_KIND * N + u] = __int_as_float(a.pinhole ? kQueryCamOrigin : 0);
+}
+
 // New samples.  A slot-wave whose 64 slots are all idle (every sample of its batch finished,
 // or the slots are fresh) pulls the next batch of 64 consecutive units -- one pixel's
 // samples: coherent rays -- from its counter shard (one 128-B line per shard), and each
@@ -1597,24 +1668,8 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
     }
     return;
   }
-  // compute_pixel_color (raytracer.cpp:18-70): one sample of pixel (px, py)
   Rng rng;
-  rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
-  const int s = a.spp_sqrt;
-  float fx, fy;
-  if (s <= 1) {
-    fx = (float)px + 0.5f;
-    fy = (float)py + 0.5f;
-  } else {
-    int si = sample % s, sj = sample / s;
-    double ox = rng.next();
-    double oy = rng.next();
-    double sx = ((double)si + ox) / (double)s;
-    double sy = ((double)sj + oy) / (double)s;
-    fx = (float)((double)px + sx);
-    fy = (float)((double)py + sy);
-  }
-  Ray ray = camera_ray(a.cam, fx, fy, rng);
+  Ray ray = sample_ray(a, px, py, sample, rng);
   ray.time = (float)rng.next();
   S[F_UNIT * N + slot] = (uint32_t)unit;
   S[F_CTRL * N + slot] = (uint32_t)ST_CLOSEST;  // depth 0
@@ -1725,6 +1780,108 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
   a.out[off + 2] = c.z;
 }
 
+// One sample of a one-pass call, from the trace launch's answer: Trace's miss colour or the
+// hit's shade with the occlusion bits the tracing lane left (raytracer.cpp:180-274, 293-303),
+// then Trace's (lc * L + r * R) + t * T with no child traced (:303-350) -- the logic step's ops
+// for these states, in its order (point lights: one shadow ray each, vis = count / 1).
+template <bool kTex>
+__device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit) {
+  const int res = a.result[unit];
+  if (res < 0) return V3{0.1f, 0.1f, 0.1f};
+  const HitRec hr = load_hit(hit_rec_u(a.hit, unit));
+  const V3 hp = hr.p, hn = hr.n;
+  const rt_material& m = a.mats[hr.mat];
+  float hu = 0.0f, hv = 0.0f;
+  if (kTex) {
+    const float2 uv = a.hit_uv[unit];
+    hu = uv.x;
+    hv = uv.y;
+  }
+  const V3 base0 = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+  V3 fin{base0.x * m.k_ambient, base0.y * m.k_ambient, base0.z * m.k_ambient};
+  if (a.n_fuse > 0) {
+    const unsigned occl_bits = a.occl[unit];
+    const size_t N = (size_t)(unsigned)a.n_slots;
+    const V3 ro = a.pinhole ? V3{a.cam.location[0], a.cam.location[1], a.cam.location[2]}
+                            : V3{a.query[(Q_O + 0) * N + unit], a.query[(Q_O + 1) * N + unit],
+                                 a.query[(Q_O + 2) * N + unit]};
+    for (int light = 0; light < a.n_lights; ++light) {
+      const rt_light& L = a.lights[light];
+      float vis = 0.0f;
+      if (!((occl_bits >> light) & 1u)) vis += 1.0f;
+      vis = vis / (float)1;  // ns = 1 (radius 0)
+      if (!(vis <= 0.0f)) {
+        V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+        V3 V = normalize(sub(ro, hp));
+        V3 lc = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
+        float dsq = dot(lc, lc);
+        float ldist = sqrtf(dsq);
+        V3 Ld = normalize(lc);
+        float ndl = smax(0.0f, dot(hn, Ld));
+        V3 diff = mul(base, ndl);
+        V3 H = normalize(add(Ld, V));
+        float ndh = smax(0.0f, dot(hn, H));
+        float si = rt_powf(ndh, m.shininess);
+        V3 spec{m.specular[0] * si, m.specular[1] * si, m.specular[2] * si};
+        float att = (10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq);
+        V3 inner{diff.x * m.k_diffuse + spec.x * m.k_specular, diff.y * m.k_diffuse + spec.y * m.k_specular,
+                 diff.z * m.k_diffuse + spec.z * m.k_specular};
+        V3 contrib{L.color[0] * inner.x * att, L.color[1] * inner.y * att, L.color[2] * inner.z * att};
+        fin = V3{fin.x + contrib.x * vis, fin.y + contrib.y * vis, fin.z + contrib.z * vis};
+      }
+    }
+  }
+  const float lcf = smax(0.0f, 1.0f - m.reflectivity - m.transparency);
+  const V3 A{lcf * fin.x, lcf * fin.y, lcf * fin.z};
+  const V3 part{A.x + m.reflectivity * 0.0f, A.y + m.reflectivity * 0.0f, A.z + m.reflectivity * 0.0f};
+  return V3{part.x + m.transparency * 0.0f, part.y + m.transparency * 0.0f, part.z + m.transparency * 0.0f};
+}
+
+// The one-pass call's last kernel: the logic step (one_pass_sample) and reduce_kernel in one
+// pass, with no per-sample colour buffer.  A block owns 256 pixels; each pass shades 16
+// samples of every pixel (consecutive threads take consecutive units of a pixel) into LDS,
+// then every thread adds its own pixel's in the reference's order (raytracer.cpp:46-69).
+template <bool kTex>
+__global__ __launch_bounds__(kBlock) void shade_reduce_kernel(LogicArgs a) {
+  __shared__ float stage[kBlock * kRedStride];
+  const int p0 = blockIdx.x * kBlock;
+  const int np = min(kBlock, a.n_pixels - p0);
+  const int p = p0 + (int)threadIdx.x;
+  const int ns = a.n_samples;
+  V3 acc{0.0f, 0.0f, 0.0f};
+  for (int s0 = 0; s0 < ns; s0 += kRedChunk) {
+    const int cn = min(kRedChunk, ns - s0);
+    for (int i = (int)threadIdx.x; i < np * cn; i += kBlock) {
+      const int j = cn == kRedChunk ? i / kRedChunk : i / cn, k = i - j * cn;
+      const V3 c = one_pass_sample<kTex>(a, (size_t)(p0 + j) * (size_t)ns + (size_t)(s0 + k));
+      float* d = stage + j * kRedStride + k * 3;
+      d[0] = c.x;
+      d[1] = c.y;
+      d[2] = c.z;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      const float* q = stage + threadIdx.x * kRedStride;
+      if (a.spp_sqrt <= 1) acc = V3{q[0], q[1], q[2]};
+      else
+        for (int k = 0; k < cn * 3; k += 3) acc = V3{acc.x + q[k], acc.y + q[k + 1], acc.z + q[k + 2]};
+    }
+    __syncthreads();
+  }
+  if (p >= a.n_pixels) return;
+  int x, y;
+  size_t off;
+  if (!pixel_coords(a, p, x, y, off)) return;
+  V3 c = acc;
+  if (a.spp_sqrt > 1) {  // compute_pixel_color: sum / (float)(s*s) (raytracer.cpp:46-69)
+    const float tot = (float)a.n_samples;
+    c = V3{acc.x / tot, acc.y / tot, acc.z / tot};
+  }
+  a.out[off] = c.x;
+  a.out[off + 1] = c.y;
+  a.out[off + 2] = c.z;
+}
+
 // pixel finalisation (raytracer.cpp:446-457, image.cpp:28-37), the same ops as rth_quantise
 __global__ __launch_bounds__(kBlock) void quantise_kernel(const float* rgb, long long n, uint8_t* out) {
   const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
@@ -1768,7 +1925,8 @@ template <bool kCount>
 void launch_trace2(const TraceArgs& ta, bool planes, bool soft, unsigned blocks, size_t lds, hipStream_t st) {
   if (ta.n_fuse > 0 && planes)  // point lights only (the host's choice)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-  else if (ta.n_fuse > 0)  // ... and no textures: the fused path stores no (u, v)
+  else if (ta.n_fuse > 0 || ta.one_pass)  // ... and no textures: the fused path stores no (u, v); one-pass
+                                          // calls of transformed shapes: the lane computes the hit record
     hipLaunchKernelGGL((trace_refill_kernel<kCount, false, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (soft && planes)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
@@ -1874,18 +2032,20 @@ struct rt_scene_s {
   void* d_ctl = nullptr;  // bytes 16/24: box/prim tests, 32: rays (u64), 240..: diagnostics, 488: node visits
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
+  // (each array grown on demand by grow(); its byte capacity beside it: a one-pass call needs
+  // only the query record, result, hit record and occlusion bits of its slots)
   uint32_t* d_state = nullptr;
   uint32_t* d_frames = nullptr;
   float* d_refr = nullptr;
   float* d_query = nullptr;
   float* d_samples = nullptr;
-  size_t samples_cap = 0;
   int* d_result = nullptr;
   float* d_hit = nullptr;
   unsigned int* d_occl = nullptr;  // per slot: occlusion bits of fused shadow rays
   float2* d_hit_uv = nullptr;      // per slot: (u, v) of the closest hit (textured scenes)
   unsigned int* d_wave_done = nullptr;
-  size_t slots_cap = 0;
+  size_t cap_state = 0, cap_frames = 0, cap_refr = 0, cap_query = 0, cap_samples = 0, cap_result = 0, cap_hit = 0,
+         cap_occl = 0, cap_hit_uv = 0, cap_wave_done = 0;
   unsigned int* h_flag = nullptr;  // pinned: per pipeline, one 128-B line per step of a host batch (any_query copies)
   unsigned long long* h_stats = nullptr;  // pinned: the first kStatsBytes of the control block, copied after each batch
   std::vector<int32_t> tiles_on_device;   // the tile list d_tiles holds
@@ -1914,8 +2074,20 @@ static void free_workspace(rt_scene_s* s) {
   s->d_hit_uv = nullptr;
   s->d_state = nullptr; s->d_frames = nullptr; s->d_refr = nullptr;
   s->d_query = nullptr; s->d_result = nullptr; s->d_samples = nullptr; s->d_hit = nullptr;
-  s->slots_cap = 0;
-  s->samples_cap = 0;
+  s->cap_state = s->cap_frames = s->cap_refr = s->cap_query = s->cap_samples = s->cap_result = s->cap_hit = 0;
+  s->cap_occl = s->cap_hit_uv = s->cap_wave_done = 0;
+}
+
+// A workspace array of at least `bytes` (contents undefined): reallocated only to grow.
+template <class T>
+static int grow(T*& ptr, size_t& cap, size_t bytes) {
+  if (ptr && bytes <= cap) return RT_OK;
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  cap = 0;
+  HIP_TRY(hipMalloc((void**)&ptr, std::max<size_t>(bytes, 4)), RT_ENOMEM);
+  cap = std::max<size_t>(bytes, 4);
+  return RT_OK;
 }
 
 // Render order of a call's tiles: costliest first.  A launch ends when its slowest rays do,
@@ -2179,6 +2351,36 @@ int rt_tile_costs(rt_scene_t s, const rt_camera_desc* cam, int32_t tile_w, int32
   return RT_OK;
 }
 
+}  // extern "C"
+
+// One-pass calls: camera_kernel -> one trace launch -> shade_reduce_kernel, slot == unit and no
+// slot state.  The scene must need nothing between a sample's camera ray and its colour but the
+// closest hit and one shadow ray per light, traced by the tracing lane: no Trace recursion
+// (reflection / refraction), lights all points (the fused shadow rays: at most 24) or none,
+// and the hit's (u, v) from the trace kernel (planes) or no texture.  RT_ONE_PASS=0 turns it
+// off; an explicit RT_SLOTS / RT_PIPES / RT_FUSE (the step pipeline's knobs) or a diagnostic mode that
+// waits on every step (RT_DIAG, RT_TRACE_REPLAY) selects the step pipeline too.
+static bool one_pass_scene(const rt_scene_s* s) {
+  const bool frames = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
+  const bool tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
+  return !frames && !s->soft_lights && (s->desc.n_lights == 0 || s->fuse_lights == s->desc.n_lights) &&
+         (s->desc.prim_stride == 64 || !tex);
+}
+static bool one_pass_env() {
+  if (const char* e = std::getenv("RT_ONE_PASS")) return std::atoi(e) != 0;
+  return !std::getenv("RT_SLOTS") && !std::getenv("RT_PIPES") && !std::getenv("RT_FUSE") && !std::getenv("RT_DIAG") &&
+         !std::getenv("RT_TRACE_REPLAY");
+}
+// units of one one-pass call (larger calls run as tile chunks): 52 B of workspace per unit
+// touched (query direction 12, result 4, hit record 32 on a hit, occlusion bits 4)
+static long long one_pass_cap() {
+  long long cap = 1LL << 30;
+  if (const char* e = std::getenv("RT_ONE_PASS_MAX")) cap = std::max(1LL, std::min(cap, std::atoll(e)));
+  return cap;
+}
+
+extern "C" {
+
 int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
                     int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
                     rt_stats* stats) {
@@ -2199,9 +2401,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     const long long per_tile = (long long)tile_w * tile_h * (p->spp_sqrt <= 1 ? 1LL : (long long)p->spp_sqrt * p->spp_sqrt);
     long long cap = 1LL << 30;
     if (const char* e = std::getenv("RT_MAX_UNITS")) cap = std::max(1LL, std::min(cap, std::atoll(e)));
+    if (one_pass_scene(s) && one_pass_env()) cap = std::min(cap, one_pass_cap());
     if (n_tiles > 1 && (long long)n_tiles * per_tile > cap) {
       const int k = (int)std::max(1LL, std::min<long long>(n_tiles, cap / per_tile));
       rt_stats acc{};
+      acc.path = RT_PATH_ONE_PASS;
       for (int t0 = 0; t0 < n_tiles; t0 += k) {
         rt_stats st{};
         const int rc = rt_render_tiles(s, cam, p, tile_ids + t0, std::min(k, n_tiles - t0), tile_w, tile_h,
@@ -2215,6 +2419,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
         acc.trace_ms += st.trace_ms;
         acc.trace_busy_ms += st.trace_busy_ms;
         acc.iterations += st.iterations;
+        if (st.path != RT_PATH_ONE_PASS) acc.path = RT_PATH_STEPS;
       }
       if (stats) *stats = acc;
       return RT_OK;
@@ -2241,8 +2446,22 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // 16M (C4: 8M 13043, 16M 13065, 32M 12791: their slots carry the Trace frames and take many
   // short steps).  ~180 B of HBM per slot: 128M slots ~23 GB.
   const bool frames_scene = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
+  const bool tex_scene = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
+#ifdef RT_EXIT_TIMING
+  const bool one_pass = false;
+#else
+  const bool one_pass = one_pass_scene(s) && one_pass_env() && n_units <= one_pass_cap();
+#endif
   long long slots = frames_scene ? std::min(n_units, 16LL << 20) : std::min(n_units, 128LL << 20);
   if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
+  // slot-state words are addressed S[field * N + slot] in 32-bit int: (highest field + 1) * N
+  // <= 2^31.  Scenes without Trace frames touch fields up to F_RAY + 2 (the ray origin), scenes
+  // with frames all F_COUNT; RT_SLOTS is clamped to that bound (one-pass calls keep no slot
+  // state and address their arrays with 64-bit offsets)
+  static_assert((long long)(F_RAY + 3) * (128LL << 20) <= (1LL << 31), "default slot cap overflows the state index");
+  static_assert((long long)F_COUNT * (16LL << 20) <= (1LL << 31), "frames-scene slot cap overflows the state index");
+  slots = std::min(slots, ((1LL << 31) / (frames_scene ? F_COUNT : F_RAY + 3)) / kBlock * kBlock);
+  if (one_pass) slots = n_units;  // every unit its own slot
   const int n_slots = (int)(((std::min<long long>(n_units, slots) + kBlock - 1) / kBlock) * kBlock);
   if ((size_t)n_tiles > s->tiles_cap) {  // render-order tile ids, then their output positions
     if (s->d_tiles) (void)hipFree(s->d_tiles);
@@ -2252,26 +2471,22 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_tiles, (size_t)n_tiles * 2 * sizeof(int32_t)), RT_ENOMEM);
     s->tiles_cap = (size_t)n_tiles;
   }
-  if ((size_t)n_slots > s->slots_cap || (need_frames && !s->d_frames) || (need_refr && !s->d_refr)) {
-    free_workspace(s);
-    size_t N = (size_t)std::max(n_slots, 1);
-    HIP_TRY(hipMalloc(&s->d_state, N * F_COUNT * 4), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_query, N * Q_COUNT * 4), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_result, N * 4), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_hit, N * HIT_STRIDE * 4), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_hit_uv, N * sizeof(float2)), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_occl, N * 4), RT_ENOMEM);
-    HIP_TRY(hipMalloc(&s->d_wave_done, (N / 64 + 1) * 4), RT_ENOMEM);
-    if (need_frames) HIP_TRY(hipMalloc(&s->d_frames, N * kMaxDepth * FR_COUNT * 4), RT_ENOMEM);
-    if (need_refr) HIP_TRY(hipMalloc(&s->d_refr, N * kMaxDepth * 6 * 4), RT_ENOMEM);
-    s->slots_cap = N;
-  }
-  if ((size_t)n_units * 3 > s->samples_cap) {
-    if (s->d_samples) (void)hipFree(s->d_samples);
-    s->d_samples = nullptr;
-    s->samples_cap = 0;
-    HIP_TRY(hipMalloc(&s->d_samples, (size_t)n_units * 3 * sizeof(float)), RT_ENOMEM);
-    s->samples_cap = (size_t)n_units * 3;
+  {
+    const size_t N = (size_t)std::max(n_slots, 1);
+    int rc = RT_OK;
+    if ((rc = grow(s->d_query, s->cap_query, N * Q_COUNT * 4)) || (rc = grow(s->d_result, s->cap_result, N * 4)) ||
+        (rc = grow(s->d_hit, s->cap_hit, N * HIT_STRIDE * 4)) ||
+        (tex_scene && (rc = grow(s->d_hit_uv, s->cap_hit_uv, N * sizeof(float2)))) ||
+        (s->fuse_lights > 0 && (rc = grow(s->d_occl, s->cap_occl, N * 4))))
+      return rc;
+    if (!one_pass) {  // the step pipeline's slot state, Trace frames and per-sample colours
+      if ((rc = grow(s->d_state, s->cap_state, N * F_COUNT * 4)) ||
+          (rc = grow(s->d_wave_done, s->cap_wave_done, (N / 64 + 1) * 4)) ||
+          (need_frames && (rc = grow(s->d_frames, s->cap_frames, N * kMaxDepth * FR_COUNT * 4))) ||
+          (need_refr && (rc = grow(s->d_refr, s->cap_refr, N * kMaxDepth * 6 * 4))) ||
+          (rc = grow(s->d_samples, s->cap_samples, (size_t)n_units * 3 * sizeof(float))))
+        return rc;
+    }
   }
   // render order and the tile list in that order + output positions; uploaded only when it
   // changed (a renderer's frames reuse one list).  Costliest tiles first for a call whose
@@ -2377,7 +2592,10 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   ta.leaf_min = leaf_min_env();
   ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
   // free lanes help the queries still traversing once a launch's queue is dry (RT_DRAIN_HELP=0 off)
-  ta.drain_help = 1;
+  // The instrumented (count_work) frame runs without helpers: a helper searches a subtree under
+  // a bound that lags its owner's, so its visits depend on scheduling; without them the counts
+  // are the serial near-first traversal's (the algorithmic bytes bench.py reports)
+  ta.drain_help = p->count_work ? 0 : 1;
   if (const char* e = std::getenv("RT_DRAIN_HELP")) ta.drain_help = std::atoi(e) != 0 ? 1 : 0;
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
@@ -2399,7 +2617,16 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   if (const char* e = std::getenv("RT_FUSE")) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
   // the launched instance (launch_trace2): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
   // entries except fused shadows over transformed shapes (5, 16)
-  const bool fuse_launch = ta.n_fuse > 0, soft_launch = !fuse_launch && soft_trace;
+  ta.one_pass = one_pass ? 1 : 0;
+  ta.op_time = planes_only ? 0 : 1;  // a plane ignores the ray time (a moving sphere needs it)
+  la.op_time = ta.op_time;
+  {  // some tile reaches past the image: its outside units are marked in the kind word
+    bool edge = false;
+    for (int i = 0; i < n_tiles && !edge; ++i)
+      edge = ((tile_ids[i] % tiles_x) + 1) * tile_w > cam->res_x || ((tile_ids[i] / tiles_x) + 1) * tile_h > cam->res_y;
+    ta.op_kind = la.op_kind = edge ? 1 : 0;
+  }
+  const bool fuse_launch = ta.n_fuse > 0 || (one_pass && !planes_only), soft_launch = !fuse_launch && soft_trace;
   const bool six_waves = !(fuse_launch && !planes_only);
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(six_waves));
   ta.occl = s->d_occl;
@@ -2431,7 +2658,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // 7683 -- one by default, RT_PIPES=2..4 on request.
   int n_pipes = n_units <= (4LL << 20) ? 1 : pipes_env();
   if (const char* e = std::getenv("RT_PIPES")) n_pipes = pipes_env();  // an explicit request holds for any size
-  if (step_sync) n_pipes = 1;
+  if (step_sync || one_pass) n_pipes = 1;
   n_pipes = std::max(1, std::min(n_pipes, n_slots / kBlock));  // every pipeline gets whole blocks of slots
   struct Pipe {
     LogicArgs la;
@@ -2535,7 +2762,36 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
     return RT_OK;
   };
-  for (int live = n_pipes; live > 0;) {
+  if (one_pass) {  // camera rays, one trace launch, shading + reduction: one host wait
+    Pipe& P = pipes[0];
+    unsigned int* aq = P.ta.fetch + (size_t)ta.fetch_shards * kFetchStride;  // cleared by init_kernel
+    P.la.any_query = aq;
+    P.ta.any_query = aq;
+    P.ta.host_flag = s->h_flag;
+    P.ta.n_work = (int)n_units;
+    hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
+    launch_trace(P.ta, p->count_work != 0, planes_only, false, P.trace_blocks, lds, stream);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
+    const unsigned rblocks = (unsigned)((n_pixels + kBlock - 1) / kBlock);
+    if (tex) hipLaunchKernelGGL(shade_reduce_kernel<true>, dim3(rblocks), dim3(kBlock), 0, stream, la);
+    else hipLaunchKernelGGL(shade_reduce_kernel<false>, dim3(rblocks), dim3(kBlock), 0, stream, la);
+    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    if (stats) HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
+    HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
+    float ms = 0.f, t_a = 0.f, t_b = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[0][0], s->ev_b[0][0]), RT_EDEVICE);
+    if (stats && hipEventElapsedTime(&t_a, s->ev_t0, s->ev_a[0][0]) == hipSuccess &&
+        hipEventElapsedTime(&t_b, s->ev_t0, s->ev_b[0][0]) == hipSuccess)
+      busy.emplace_back(t_a, t_b);
+    trace_ms = ms;
+    iters = P.iters = 1;
+    reduced = true;
+  }
+  for (int live = one_pass ? 0 : n_pipes; live > 0;) {
     for (int h = 0; h < n_pipes; ++h) {
       Pipe& P = pipes[h];
       if (P.done) continue;
@@ -2677,6 +2933,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     if (cur_b > cur_a) un += cur_b - cur_a;
     stats->trace_busy_ms = un;
     stats->iterations = iters;
+    stats->path = one_pass ? RT_PATH_ONE_PASS : RT_PATH_STEPS;
 #ifdef RT_PHASE_TIMING
     {
       unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};

@@ -28,8 +28,6 @@
 #include <thread>
 #include <utility>
 #include <stdexcept>
-#include <system_error>
-#include <thread>
 #include <vector>
 
 #include "scene.hpp"

@@ -10,6 +10,8 @@
 // Built with -ffp-contract=off: every float op keeps the reference's order and rounding.
 #include "scene.hpp"
 
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -455,9 +457,30 @@ void BuildTimer::lap(const char* phase) {
   last = t;
 }
 
+// Cores this process may use: its affinity mask capped by the cgroup v2 CPU quota (the job's
+// share on a shared host; hardware_concurrency() is the whole machine) -- bench.py's usable_cpus()
+static int usable_cores() {
+  int n = 0;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+  if (n <= 0) {
+    const unsigned hc = std::thread::hardware_concurrency();
+    n = hc ? (int)hc : 1;
+  }
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long per = 0;
+    if (std::fscanf(f, "%31s %lld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+      const long long quota = std::atoll(q) / per;
+      if (quota >= 1) n = (int)std::min<long long>(n, quota);
+    }
+    std::fclose(f);
+  }
+  return std::max(1, n);
+}
+
 int build_threads() {
-  const unsigned hc = std::thread::hardware_concurrency();
-  const int cores = std::max(1, (int)(hc ? hc : 1));
+  const int cores = usable_cores();
   if (const char* e = std::getenv("RT_BUILD_THREADS")) return std::max(1, std::min(std::min(64, cores), std::atoi(e)));
   return std::min(16, cores);
 }

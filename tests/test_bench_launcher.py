@@ -1,0 +1,55 @@
+"""bench.py's rank launcher (CPU): `bench.py --gpus N` started directly must run N ranks --
+the driver's `python bench.py --gpus 1` form, and the same form with N > 1, may not silently
+measure one GPU -- and an external launcher's WORLD_SIZE must agree with --gpus.
+
+--dry-run stops after the process group is up (gloo) and one all-reduce has counted the
+ranks, so the real torch.distributed.run child and rendezvous run here without a GPU.  The
+rendering side of the N-rank path is tests/test_bench_ranks.py (GPU).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_plan_without_launcher():
+    assert bench.launch_plan(None, {}) == ("run", 1)
+    assert bench.launch_plan(1, {}) == ("run", 1)
+    assert bench.launch_plan(4, {}) == ("spawn", 4)
+    assert bench.launch_plan(0, {})[0] == "error"
+
+
+def test_plan_under_launcher():
+    assert bench.launch_plan(None, {"WORLD_SIZE": "8"}) == ("run", 8)
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}) == ("run", 8)
+    how, msg = bench.launch_plan(8, {"WORLD_SIZE": "1"})
+    assert how == "error" and "WORLD_SIZE=1" in msg and "--gpus 8" in msg
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_gpus_flag_spawns_ranks(n):
+    r = _run(["--gpus", str(n), "--dry-run"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["ranks_in_group"] == n
+
+
+def test_world_size_mismatch_fails():
+    r = _run(["--gpus", "8", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr and r.stdout.strip() == ""

@@ -2,10 +2,13 @@
 device buffers, the gather to rank 0 and the unpack must give the same frame, bit for bit, as
 one rank rendering every tile (the counter RNG is keyed by pixel/sample, not by rank).
 
-The ranks share the one GPU of the test box and gather through gloo (RT_BENCH_BACKEND=gloo):
+`bench.py --gpus N` is started directly, as the driver does: it spawns its N ranks (a child
+torch.distributed.run) and the JSON line must say n_gpus N.  The ranks share the one GPU
+of the test box and gather through gloo (RT_BENCH_BACKEND=gloo):
 this exercises everything bench.py does for N > 1 except the RCCL transport itself, which
 tests/test_comm.py and the driver's multi-GPU runs cover.
 """
+import json
 import os
 import subprocess
 import sys
@@ -21,14 +24,15 @@ SMALL = ["--tris", "20000", "--res", "320", "--spp-sqrt", "3", "--tile", "64", "
 def _bench(tmp_path, n, tag):
     frame = str(tmp_path / f"frame_{tag}.npy")
     env = dict(os.environ, RT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    if n == 1:
-        cmd = [sys.executable, "bench.py"]
-    else:
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-               "--master-addr", "127.0.0.1", "--master-port", str(29600 + n), "bench.py", "--gpus", str(n)]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    # the driver's form: `bench.py --gpus N` started directly spawns its N ranks
+    cmd = [sys.executable, "bench.py", "--gpus", str(n)]
     r = subprocess.run(cmd + SMALL + ["--dump-frame", frame], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == n
     return np.load(frame)
 
 

@@ -7,7 +7,7 @@ many work-counter shards, a slot count so small that a frame takes dozens of ste
 slots split into two pipelines on two streams, soft-shadow samples advanced by
 shadow_step_kernel or by the logic kernel instead of the tracing lane, the greedy BVH4
 collapse instead of the SAH-optimal one, point-light shadow rays left unfused in a small
-call, one or four slot pipelines instead of the default two, and the tiles rendered in the
+call, two or four slot pipelines instead of the default one, and the tiles rendered in the
 caller's order instead of costliest first (small calls' default), and the lanes still
 traversing when a launch's queue runs dry left alone instead of helped by the free lanes.
 """
@@ -49,7 +49,7 @@ KNOBS = [
     {"RT_SOFT_FUSE": "0", "RT_SHADOW_STEP": "0"},  # ... or by the logic kernel itself
     {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
     {"RT_FUSE": "0"},  # point-light shadow rays as their own queries (small calls fuse them by default)
-    {"RT_PIPES": "1"},  # one slot pipeline (the default is two on two streams)
+    {"RT_PIPES": "2"},  # two slot pipelines on two streams (the default is one)
     {"RT_TILE_ORDER": "0"},  # tiles in the caller's order (small calls render costliest tiles first)
     {"RT_PIPES": "4", "RT_SLOTS": "8192"},  # four pipelines of two slot blocks each
     {"RT_DRAIN_HELP": "0"},  # no drain helpers: each query traversed by its own lane alone

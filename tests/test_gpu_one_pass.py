@@ -1,0 +1,110 @@
+"""One-pass calls against the oracle: camera_kernel writes every unit's camera ray, one trace
+launch answers every closest query and the fused point-light shadow rays, and
+shade_reduce_kernel shades each sample and sums each pixel -- no slot state, no logic steps.
+
+Eligible scenes: no Trace recursion (reflectivity = transparency = 0), lights all points or
+none, textures on planes only.  Each case renders through the default path (asserted to be
+one-pass: rt_stats.path), through the step pipeline (RT_ONE_PASS=0) and as many one-pass tile
+chunks (RT_ONE_PASS_MAX), and every float must equal the oracle's (counter RNG) with equal
+ray counts.  The cases cover what the one-pass path branches on: planes with and without
+lights (plain / fused trace instances), the c3 == c2 unbounded list, textured planes (the
+hit's (u, v) from the trace kernel), transformed shapes with lights and without (the fused
+instance computing the hit record alone), a moving sphere (the ray time), a thin-lens
+camera (stored origins), tiles reaching past the image (the kind word), several lights.
+Reference: Code/raytracer.cpp:18-70 (compute_pixel_color), :180-274 (shade), :280-351 (Trace).
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import ray_tracying_amd as rt
+import scenes
+
+pytestmark = pytest.mark.gpu
+SEED = 424242
+
+
+def _flat(sc: dict) -> dict:
+    """features() without reflection / refraction / soft lights / textures: one-pass eligible."""
+    sc = copy.deepcopy(sc)
+    for kind in ("spheres", "cubes", "rectangles", "planes"):
+        for o in sc.get(kind, []):
+            m = o.get("material")
+            if m:
+                m["reflectivity"] = 0.0
+                m["transparency"] = 0.0
+                m.pop("texture_file", None)
+    for light in sc["lights"]:
+        light["radius"] = 0.0
+    return sc
+
+
+def _textured_soup():
+    sc = scenes.soup(1500, seed=21, res=(40, 40))
+    for k, pl in enumerate(sc["planes"]):
+        if k % 3 == 0:
+            pl["material"] = {"diffuse_color": [0.9, 0.8, 0.7], "texture_file": "checker.jpg"}
+    return sc
+
+
+def _multi_light_soup():
+    sc = scenes.soup(2000, seed=8, res=(48, 40))
+    sc["lights"] += [{"location": [-2.0, -2.5, 1.0], "intensity": 300.0, "color": [0.4, 0.6, 1.0], "radius": 0.0},
+                     {"location": [0.0, 0.0, 0.0], "intensity": 50.0, "color": [1.0, 0.2, 0.2]}]
+    return sc
+
+
+CASES = {
+    "soup_lit": (lambda: scenes.soup(3000, seed=11, res=(96, 72)), 2),
+    "soup_dark": (lambda: scenes.soup(3000, seed=12, res=(64, 64), light=False), 1),
+    "soup_degenerate": (lambda: scenes.soup_degenerate(res=(48, 40)), 2),
+    "soup_textured": (_textured_soup, 2),
+    "soup_three_lights": (_multi_light_soup, 2),
+    "shapes_lit": (lambda: _flat(scenes.features(res=(136, 72))), 2),
+    "shapes_dark": (lambda: {**_flat(scenes.features(res=(40, 32))), "lights": []}, 1),
+    "shapes_thin_lens": (lambda: _flat(scenes.features(res=(40, 32), aperture=0.4, focus=5.0)), 2),
+    "antialiasing": (lambda: scenes.blend("Antialiasing", (72, 48)), 3),
+}
+
+
+def _render(path, spp_sqrt, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    sc = rt.Scene(path, texture_root=scenes.TEXTURES)
+    try:
+        return sc.render(rt.RenderParams(spp_sqrt=spp_sqrt, light_samples=1, use_bvh=True, seed=SEED))
+    finally:
+        sc.close()
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_one_pass_matches_oracle(name, tmp_path, gpu):
+    build, spp_sqrt = CASES[name]
+    path = scenes.write(build(), str(tmp_path / f"{name}.json"))
+    ref, _, ost = ob.render(path, rng=ob.RNG_COUNTER, seed=SEED, spp_sqrt=spp_sqrt, light_samples=1, use_bvh=True,
+                            texture_root=scenes.TEXTURES)
+    # one 64x64 tile per one-pass chunk (rth_render's tiles; frames wider than a tile run several)
+    chunk = str(64 * 64 * spp_sqrt * spp_sqrt)
+    for env, path_kind in (({}, rt.PATH_ONE_PASS), ({"RT_ONE_PASS": "0"}, rt.PATH_STEPS),
+                           ({"RT_ONE_PASS_MAX": chunk}, rt.PATH_ONE_PASS)):
+        img, st = _render(path, spp_sqrt, env)
+        assert st.path == path_kind, (name, env, st.path)
+        bad = int((img.view(np.uint32) != ref.view(np.uint32)).sum())
+        assert bad == 0, f"{name} {env}: {bad} channels differ from the oracle"
+        assert st.rays == ost["rays"], (name, env, st.rays, ost["rays"])
+
+
+def test_ineligible_scenes_take_the_step_pipeline(tmp_path, gpu):
+    """Reflection / refraction / soft lights keep the step pipeline (their samples draw and
+    branch after the camera ray)."""
+    path = scenes.write(scenes.features(res=(24, 16)), str(tmp_path / "f.json"))
+    _, st = _render(path, 1, {})
+    assert st.path == rt.PATH_STEPS
