@@ -412,8 +412,10 @@ def main():
     trace_ms = 0.0
     busy_ms = 0.0
     launches = 0
+    one_pass = True
     for k in range(args.steps):
         st = step(args.seed + k)
+        one_pass = one_pass and st.path == rt.PATH_ONE_PASS
         rays += st.rays
         trace_ms += st.trace_ms
         busy_ms += st.trace_busy_ms
@@ -548,6 +550,8 @@ def main():
             "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample {args.light_samples}",
             "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}" + (f" ({args.deal} deal)" if split > 1 else ""),
             "rng": "counter (splitmix64 per pixel/sample)",
+            "pipeline": ("one-pass (camera_kernel -> one trace_refill_kernel launch -> shade_reduce_kernel)" if one_pass
+                         else "steps (logic -> start -> trace over slot state, then reduce)"),
             **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),
         },
         "roofline": roofline,

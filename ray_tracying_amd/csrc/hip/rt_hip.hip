@@ -192,6 +192,9 @@ struct LogicArgs {
   rt_camera_desc cam;
   int spp_sqrt, light_samples;
   uint64_t seed_key;
+  FastDiv fd_s;                 // sample -> (sj, si): division by spp_sqrt
+  double inv_s;                 // RN(1 / spp_sqrt): the jitter's quotients (rt_div_by)
+  float inv_res_x, inv_res_y;   // RN(1 / res): the camera's pixel -> NDC quotients
   // work
   const int* tile_ids;         // the call's tiles in render order (costliest first, see tile_cost_order)
   const int* tile_out;         // render-order index -> the caller's index (output position); null: identity
@@ -378,6 +381,16 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
   }
 }
 
+// cswap on non-negative (or +inf) floats compared as integers (RT_INT_CULL A/B build)
+__device__ __forceinline__ void cswap_bits(float& ta, int& ca, float& tb, int& cb) {
+  const int ia = __float_as_int(ta), ib = __float_as_int(tb);
+  const bool sw = ib < ia;
+  ta = __int_as_float(sw ? ib : ia);
+  tb = __int_as_float(sw ? ia : ib);
+  const int c = sw ? cb : ca;
+  cb = sw ? ca : cb;
+  ca = c;
+}
 __device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
   const bool sw = tb < ta;
   const float t = sw ? tb : ta;
@@ -634,6 +647,21 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   // t_near <= t_far, t_far >= 0 and t_near <= lim; misses sort last as (inf, entry)
   float t[4];
   int c[4];
+#ifdef RT_INT_CULL
+  // the same test on the values' bit patterns as signed integers (A/B build): for floats >= +0
+  // integer order is float order, a negative float is a negative integer, so
+  // max(tnx, tny, tnz, 0) is exact and a negative far distance still fails the test (its
+  // value no longer matters); a far distance of exactly -0 now fails too -- conservative, as
+  // no accepted hit lies there (the origin would sit on a padded box's far face)
+  const int lim_b = __float_as_int(lim);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int nb = max(max(__float_as_int(tnx[k]), __float_as_int(tny[k])), max(__float_as_int(tnz[k]), 0));
+    const int fb = min(min(__float_as_int(tfx[k]), __float_as_int(tfy[k])), min(__float_as_int(tfz[k]), lim_b));
+    t[k] = __int_as_float(nb <= fb ? nb : 0x7f800000);
+    c[k] = cc[k];
+  }
+#else
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const float n0 = fmaxf(fmaxf(tnx[k], tny[k]), fmaxf(tnz[k], 0.0f));
@@ -641,6 +669,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     t[k] = n0 <= f0 ? n0 : __builtin_inff();
     c[k] = cc[k];
   }
+#endif
   // Order the four (t, entry) pairs just enough: three compare-exchanges put the nearest
   // first (the lane's next item), the pushes below need no order among the other three.  A
   // full sort (5, RT_SORT_SWAPS A/B build) visits 0.7 % fewer nodes but costs 10 VALU more per
@@ -648,12 +677,20 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #ifndef RT_SORT_SWAPS
 #define RT_SORT_SWAPS 3
 #endif
+#ifdef RT_INT_CULL  // the t values are >= +0 or +inf: integer order on their bits
+  cswap_bits(t[0], c[0], t[1], c[1]);
+  cswap_bits(t[2], c[2], t[3], c[3]);
+  cswap_bits(t[0], c[0], t[2], c[2]);
+  const bool v3 = __float_as_int(t[3]) != 0x7f800000, v2 = __float_as_int(t[2]) != 0x7f800000,
+             v1 = __float_as_int(t[1]) != 0x7f800000;
+#else
   cswap(t[0], c[0], t[1], c[1]);
   cswap(t[2], c[2], t[3], c[3]);
   cswap(t[0], c[0], t[2], c[2]);
   if (RT_SORT_SWAPS >= 4) cswap(t[1], c[1], t[3], c[3]);
   if (RT_SORT_SWAPS >= 5) cswap(t[1], c[1], t[2], c[2]);
   const bool v3 = t[3] != __builtin_inff(), v2 = t[2] != __builtin_inff(), v1 = t[1] != __builtin_inff();
+#endif
   // push the three other children (entries 3, 2, 1; far-to-near when fully sorted).  Writes
   // at sp, sp+v3, sp+v3+v2 -- offsets counting only the children entered -- leave exactly
   // those below the new top whatever the order (a missed one lands on the next slot and is
@@ -669,7 +706,11 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     if (v2) stack_push(a, S, sp, gtid, c[2], t[2]);
     if (v1) stack_push(a, S, sp, gtid, c[1], t[1]);
   }
+#ifdef RT_INT_CULL
+  if (__float_as_int(t[0]) != 0x7f800000) return c[0];
+#else
   if (t[0] != __builtin_inff()) return c[0];
+#endif
   return stack_pop_live(a, S, sp, gtid, lim);
 }
 
@@ -1113,14 +1154,17 @@ __device__ __forceinline__ V3 diffuse_color(const LogicArgs& a, const rt_materia
 }
 
 // Camera::pixelToRay_thin_lens (camera.cpp:98-179), basis precomputed on the host.
-__device__ __forceinline__ Ray camera_ray(const rt_camera_desc& c, float px, float py, Rng& rng) {
-  float nx = 1.0f - ((px) / ((float)c.res_x)) * 2.0f;
-  float ny = 1.0f - ((py) / ((float)c.res_y)) * 2.0f;
+// The divisions px / res and those of the normalisations are correctly rounded quotients by
+// a precomputed reciprocal (rt_div.h: the same bits, a third of the instructions).
+__device__ __forceinline__ Ray camera_ray(const rt_camera_desc& c, float px, float py, Rng& rng, float inv_rx,
+                                          float inv_ry) {
+  float nx = 1.0f - rt_div_by(px, (float)c.res_x, inv_rx) * 2.0f;
+  float ny = 1.0f - rt_div_by(py, (float)c.res_y, inv_ry) * 2.0f;
   float nxr = nx * c.half_sensor_w, nyr = ny * c.half_sensor_h;
   V3 dw{c.x_dir[0] * nxr + c.y_dir[0] * nyr + c.z_dir[0] * c.focal_length,
         c.x_dir[1] * nxr + c.y_dir[1] * nyr + c.z_dir[1] * c.focal_length,
         c.x_dir[2] * nxr + c.y_dir[2] * nyr + c.z_dir[2] * c.focal_length};
-  dw = normalize(dw);
+  dw = normalize_rcp(dw);
   Ray r;
   r.time = 0.0f;
   V3 loc{c.location[0], c.location[1], c.location[2]};
@@ -1142,7 +1186,7 @@ __device__ __forceinline__ Ray camera_ray(const rt_camera_desc& c, float px, flo
   V3 off{c.x_dir[0] * rx + c.y_dir[0] * ry, c.x_dir[1] * rx + c.y_dir[1] * ry,
          c.x_dir[2] * rx + c.y_dir[2] * ry};
   r.o = add(loc, off);
-  r.d = normalize(sub(fp, r.o));
+  r.d = normalize_rcp(sub(fp, r.o));
   return r;
 }
 
@@ -1574,16 +1618,16 @@ __device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, in
   if (s <= 1) {
     fx = (float)px + 0.5f;
     fy = (float)py + 0.5f;
-  } else {
-    int si = sample % s, sj = sample / s;
+  } else {  // the divisions by s: fast invariant integer division, Markstein quotients (rt_div.h)
+    const int sj = (int)fdiv((uint32_t)sample, a.fd_s), si = sample - sj * s;
     double ox = rng.next();
     double oy = rng.next();
-    double sx = ((double)si + ox) / (double)s;
-    double sy = ((double)sj + oy) / (double)s;
+    double sx = rt_div_by((double)si + ox, (double)s, a.inv_s);
+    double sy = rt_div_by((double)sj + oy, (double)s, a.inv_s);
     fx = (float)((double)px + sx);
     fy = (float)((double)py + sy);
   }
-  return camera_ray(a.cam, fx, fy, rng);
+  return camera_ray(a.cam, fx, fy, rng, a.inv_res_x, a.inv_res_y);
 }
 
 // One-pass calls (every sample of the call traced by one launch; no Trace recursion, point
@@ -1783,12 +1827,12 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
 // One sample of a one-pass call, from the trace launch's answer: Trace's miss colour or the
 // hit's shade with the occlusion bits the tracing lane left (raytracer.cpp:180-274, 293-303),
 // then Trace's (lc * L + r * R) + t * T with no child traced (:303-350) -- the logic step's ops
-// for these states, in its order (point lights: one shadow ray each, vis = count / 1).
+// for these states, in its order (point lights: one shadow ray each, vis = count / 1).  `hr`
+// is the unit's hit record (loaded by the caller; unused for a miss).
 template <bool kTex>
-__device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit) {
-  const int res = a.result[unit];
+__device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit, int res, const HitRec& hr,
+                                              unsigned occl_bits) {
   if (res < 0) return V3{0.1f, 0.1f, 0.1f};
-  const HitRec hr = load_hit(hit_rec_u(a.hit, unit));
   const V3 hp = hr.p, hn = hr.n;
   const rt_material& m = a.mats[hr.mat];
   float hu = 0.0f, hv = 0.0f;
@@ -1800,7 +1844,6 @@ __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit) {
   const V3 base0 = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
   V3 fin{base0.x * m.k_ambient, base0.y * m.k_ambient, base0.z * m.k_ambient};
   if (a.n_fuse > 0) {
-    const unsigned occl_bits = a.occl[unit];
     const size_t N = (size_t)(unsigned)a.n_slots;
     const V3 ro = a.pinhole ? V3{a.cam.location[0], a.cam.location[1], a.cam.location[2]}
                             : V3{a.query[(Q_O + 0) * N + unit], a.query[(Q_O + 1) * N + unit],
@@ -1838,37 +1881,64 @@ __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit) {
 }
 
 // The one-pass call's last kernel: the logic step (one_pass_sample) and reduce_kernel in one
-// pass, with no per-sample colour buffer.  A block owns 256 pixels; each pass shades 16
-// samples of every pixel (consecutive threads take consecutive units of a pixel) into LDS,
-// then every thread adds its own pixel's in the reference's order (raytracer.cpp:46-69).
+// pass, with no per-sample colour buffer.  A block owns 128 pixels; each pass shades 8 samples
+// of every pixel into LDS -- 1024 units, 4 per thread, their result words, occlusion bits and
+// hit records loaded together before any is used (the shading is bound by these dependent
+// loads, not by its arithmetic) -- then each pixel's thread adds its samples in the
+// reference's order (raytracer.cpp:46-69).  12.8 KB of LDS per block: 8 waves per SIMD.
+#ifndef RT_SR_PIXELS
+#define RT_SR_PIXELS 64  // r04 A/B (head / em8 / C3 Mrays/s): 128 px x 4 waves 7147 / 5850 / 27437, 64 x 6 7174 / 5901 / 28480, 64 x 8 7153 / 5904 / 28131
+#endif
+#ifndef RT_SR_WAVES
+#define RT_SR_WAVES 6
+#endif
+constexpr int kSrPixels = RT_SR_PIXELS, kSrChunk = 8, kSrStride = kSrChunk * 3 + 1;  // odd row: conflict-free sums
+constexpr int kSrUnits = kSrPixels * kSrChunk / kBlock;                     // units per thread per pass
 template <bool kTex>
-__global__ __launch_bounds__(kBlock) void shade_reduce_kernel(LogicArgs a) {
-  __shared__ float stage[kBlock * kRedStride];
-  const int p0 = blockIdx.x * kBlock;
-  const int np = min(kBlock, a.n_pixels - p0);
-  const int p = p0 + (int)threadIdx.x;
+__global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(LogicArgs a) {
+  __shared__ float stage[kSrPixels * kSrStride];
+  const int p0 = blockIdx.x * kSrPixels;
+  const int np = min(kSrPixels, a.n_pixels - p0);
   const int ns = a.n_samples;
   V3 acc{0.0f, 0.0f, 0.0f};
-  for (int s0 = 0; s0 < ns; s0 += kRedChunk) {
-    const int cn = min(kRedChunk, ns - s0);
-    for (int i = (int)threadIdx.x; i < np * cn; i += kBlock) {
-      const int j = cn == kRedChunk ? i / kRedChunk : i / cn, k = i - j * cn;
-      const V3 c = one_pass_sample<kTex>(a, (size_t)(p0 + j) * (size_t)ns + (size_t)(s0 + k));
-      float* d = stage + j * kRedStride + k * 3;
-      d[0] = c.x;
-      d[1] = c.y;
-      d[2] = c.z;
+  for (int s0 = 0; s0 < ns; s0 += kSrChunk) {
+    const int cn = min(kSrChunk, ns - s0), total = np * cn;
+    size_t u[kSrUnits];
+    int res[kSrUnits], st[kSrUnits];
+    unsigned ob[kSrUnits];
+#pragma unroll
+    for (int m = 0; m < kSrUnits; ++m) {
+      const int i = (int)threadIdx.x + m * kBlock;
+      const int j = cn == kSrChunk ? i / kSrChunk : i / cn, k = i - j * cn;
+      st[m] = j * kSrStride + k * 3;
+      u[m] = (size_t)(p0 + j) * (size_t)ns + (size_t)(s0 + k);
+      res[m] = i < total ? a.result[u[m]] : -1;
+      ob[m] = i < total && a.n_fuse > 0 ? a.occl[u[m]] : 0u;
+    }
+    HitRec hr[kSrUnits];
+#pragma unroll
+    for (int m = 0; m < kSrUnits; ++m) hr[m] = res[m] >= 0 ? load_hit(hit_rec_u(a.hit, u[m])) : HitRec{};
+#pragma unroll
+    for (int m = 0; m < kSrUnits; ++m) {
+      if ((int)threadIdx.x + m * kBlock < total) {
+        const V3 c = one_pass_sample<kTex>(a, u[m], res[m], hr[m], ob[m]);
+        float* d = stage + st[m];
+        d[0] = c.x;
+        d[1] = c.y;
+        d[2] = c.z;
+      }
     }
     __syncthreads();
     if ((int)threadIdx.x < np) {
-      const float* q = stage + threadIdx.x * kRedStride;
+      const float* q = stage + threadIdx.x * kSrStride;
       if (a.spp_sqrt <= 1) acc = V3{q[0], q[1], q[2]};
       else
         for (int k = 0; k < cn * 3; k += 3) acc = V3{acc.x + q[k], acc.y + q[k + 1], acc.z + q[k + 2]};
     }
     __syncthreads();
   }
-  if (p >= a.n_pixels) return;
+  const int p = p0 + (int)threadIdx.x;
+  if ((int)threadIdx.x >= np) return;
   int x, y;
   size_t off;
   if (!pixel_coords(a, p, x, y, off)) return;
@@ -2353,6 +2423,27 @@ int rt_tile_costs(rt_scene_t s, const rt_camera_desc* cam, int32_t tile_w, int32
 
 }  // extern "C"
 
+#ifdef RT_EXIT_TIMING
+// diagnostic build: wave start / queue-exhausted / exit times of a trace launch (100 MHz clock)
+static int print_exit_log(const TraceArgs& ta, float ms, int step) {
+  const int nw = (int)ta.n_threads / 64;
+  std::vector<unsigned long long> lg((size_t)nw * 3);
+  HIP_TRY(hipMemcpy(lg.data(), ta.exit_log, lg.size() * 8, hipMemcpyDeviceToHost), RT_EDEVICE);
+  unsigned long long b0 = ~0ull, x0 = ~0ull;
+  std::vector<double> ex;
+  for (int w = 0; w < nw; ++w) {
+    b0 = std::min(b0, lg[(size_t)w * 3]);
+    if (lg[(size_t)w * 3 + 1]) x0 = std::min(x0, lg[(size_t)w * 3 + 1]);
+  }
+  for (int w = 0; w < nw; ++w) ex.push_back((double)(lg[(size_t)w * 3 + 2] - b0) * 1e-5);  // ms
+  std::sort(ex.begin(), ex.end());
+  std::fprintf(stderr, "[rt exit] step %2d: trace %.3f ms; queue exhausted at %.3f ms; waves exit: 10%% %.3f, 50%% %.3f, 90%% %.3f, 99%% %.3f, last %.3f ms\n",
+               step, ms, x0 == ~0ull ? -1.0 : (double)(x0 - b0) * 1e-5, ex[nw / 10], ex[nw / 2], ex[nw * 9 / 10],
+               ex[nw * 99 / 100], ex[nw - 1]);
+  return RT_OK;
+}
+#endif
+
 // One-pass calls: camera_kernel -> one trace launch -> shade_reduce_kernel, slot == unit and no
 // slot state.  The scene must need nothing between a sample's camera ray and its colour but the
 // closest hit and one shadow ray per light, traced by the tracing lane: no Trace recursion
@@ -2447,11 +2538,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // short steps).  ~180 B of HBM per slot: 128M slots ~23 GB.
   const bool frames_scene = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
   const bool tex_scene = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
-#ifdef RT_EXIT_TIMING
-  const bool one_pass = false;
-#else
   const bool one_pass = one_pass_scene(s) && one_pass_env() && n_units <= one_pass_cap();
-#endif
   long long slots = frames_scene ? std::min(n_units, 16LL << 20) : std::min(n_units, 128LL << 20);
   if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
   // slot-state words are addressed S[field * N + slot] in 32-bit int: (highest field + 1) * N
@@ -2526,6 +2613,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.texels = (const uint8_t*)s->d_texels;
   la.cam = *cam;
   la.spp_sqrt = p->spp_sqrt;
+  la.fd_s = make_fastdiv((uint32_t)std::max(1, p->spp_sqrt));
+  la.inv_s = 1.0 / (double)std::max(1, p->spp_sqrt);
+  {  // volatile: the correctly rounded reciprocals of the host's IEEE division
+    volatile float rx = (float)cam->res_x, ry = (float)cam->res_y;
+    la.inv_res_x = 1.0f / rx;
+    la.inv_res_y = 1.0f / ry;
+  }
   la.light_samples = p->light_samples;
   la.seed_key = mix64_host(p->seed + 0x9E3779B97F4A7C15ull);
   la.tile_ids = s->d_tiles;
@@ -2775,7 +2869,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     launch_trace(P.ta, p->count_work != 0, planes_only, false, P.trace_blocks, lds, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
-    const unsigned rblocks = (unsigned)((n_pixels + kBlock - 1) / kBlock);
+    const unsigned rblocks = (unsigned)((n_pixels + kSrPixels - 1) / kSrPixels);
     if (tex) hipLaunchKernelGGL(shade_reduce_kernel<true>, dim3(rblocks), dim3(kBlock), 0, stream, la);
     else hipLaunchKernelGGL(shade_reduce_kernel<false>, dim3(rblocks), dim3(kBlock), 0, stream, la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
@@ -2790,6 +2884,9 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     trace_ms = ms;
     iters = P.iters = 1;
     reduced = true;
+#ifdef RT_EXIT_TIMING
+    if (const int rc = print_exit_log(P.ta, ms, 0)) return rc;
+#endif
   }
   for (int live = one_pass ? 0 : n_pipes; live > 0;) {
     for (int h = 0; h < n_pipes; ++h) {
@@ -2866,22 +2963,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
         }
         const bool more = flag[(size_t)k * kFetchStride] != 0;
 #ifdef RT_EXIT_TIMING
-        if (more) {  // wave start / queue-exhausted / exit times of this launch (100 MHz clock)
-          const int nw = (int)P.ta.n_threads / 64;
-          std::vector<unsigned long long> lg((size_t)nw * 3);
-          HIP_TRY(hipMemcpy(lg.data(), P.ta.exit_log, lg.size() * 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-          unsigned long long b0 = ~0ull, x0 = ~0ull;
-          std::vector<double> ex;
-          for (int w = 0; w < nw; ++w) {
-            b0 = std::min(b0, lg[(size_t)w * 3]);
-            if (lg[(size_t)w * 3 + 1]) x0 = std::min(x0, lg[(size_t)w * 3 + 1]);
-          }
-          for (int w = 0; w < nw; ++w) ex.push_back((double)(lg[(size_t)w * 3 + 2] - b0) * 1e-5);  // ms
-          std::sort(ex.begin(), ex.end());
-          std::fprintf(stderr, "[rt exit] step %2d: trace %.3f ms; queue exhausted at %.3f ms; waves exit: 10%% %.3f, 50%% %.3f, 90%% %.3f, 99%% %.3f, last %.3f ms\n",
-                       iters, ms, x0 == ~0ull ? -1.0 : (double)(x0 - b0) * 1e-5, ex[nw / 10], ex[nw / 2], ex[nw * 9 / 10],
-                       ex[nw * 99 / 100], ex[nw - 1]);
-        }
+        if (more) print_exit_log(P.ta, ms, iters);
 #endif
         if (diag && more) {
           unsigned long long rc = 0;

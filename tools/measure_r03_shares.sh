@@ -23,5 +23,5 @@ for r in $(seq 0 7); do
   timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --res 4096 --spp-sqrt 8 --emulate 8 --emulate-rank $r > $D/c5_8_${r}.json 2> $D/c5_8_${r}.err
   echo "c5 8-way rank $r $(python3 -c "import json;print(json.load(open('$D/c5_8_${r}.json'))['value'])")"
 done
-timeout -k 10 120 python3 tools/gather_cost.py > $D/gather_cost.json
+timeout -k 10 120 python3 tools/gather_cost.py $D/gather_cost.json > /dev/null
 python3 tools/shares_summary.py --dir $D --out gpurun_out/${L}_shares.json --label $L

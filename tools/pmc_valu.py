@@ -59,9 +59,11 @@ def main() -> None:
         "lds_per_valu": round(tot["SQ_INSTS_LDS"] / tot["SQ_INSTS_VALU"], 4),
         "per_dispatch_valu_issue_frac": [round(d["SQ_INSTS_VALU"] / (N_CU * VALU_PER_CU_CYCLE * d["GRBM_GUI_ACTIVE"] / N_XCD), 3)
                                          for d in ds],
-        "definition": "VALU issue fraction = wave64 VALU instructions / (256 CUs x cycles), one per CU-cycle peak "
-                      "(measured, tools/ubench_valu.hip); "
-                      "lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU)",
+        "definition": "valu_issue_frac = wave64 VALU instructions / (256 CUs x cycles x VALU_PER_CU_CYCLE) with "
+                      "VALU_PER_CU_CYCLE = %g (the fp32 single-opcode rate, tools/ubench_valu.hip); bench.py prices "
+                      "the roofline against the highest counter-measured mixed-stream rate instead (1.73, "
+                      "profiles/*_ubench_valu_pmc.json) and the spec 2; valu_wave_instr_per_cu_cycle is the raw "
+                      "rate; lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU)" % VALU_PER_CU_CYCLE,
     }
     with open(a.out, "w") as fh:
         json.dump(res, fh, indent=1)

@@ -4,7 +4,8 @@
 For an N-way split every rank renders its lattice share alone on one GPU; with one GPU per
 rank the frame takes the slowest rank's time plus the gather.  Predicted N-GPU Mrays/s =
 whole-frame rays / (max over ranks of the share's ms per frame + gather estimate); speed-up =
-that / the whole frame's Mrays/s on one GPU."""
+that / the whole frame's Mrays/s on one GPU.  The gather term is the measured fixed cost of one
+RCCL gather at world size 1 plus the payload over one xGMI link (tools/gather_cost.py)."""
 import argparse
 import glob
 import json
@@ -33,7 +34,10 @@ for wl in ("head", "c5"):
         ranks = [J(p) for p in files]
         ms = [r["ms_per_step"] for r in ranks]
         g = gather.get(f"{wl}_{n}way", {})
-        g_ms = g.get("xgmi_estimate_ms") or 0.0  # every peer arrives over its own link, concurrently
+        # the collective's fixed cost (one torch.distributed.gather over RCCL at world size 1,
+        # synchronised like bench.py's step) + the payload over one xGMI link (every peer
+        # arrives over its own link, concurrently)
+        g_ms = (g.get("gather_ms") or 0.0) + (g.get("xgmi_est_ms") or g.get("xgmi_estimate_ms") or 0.0)
         slow = max(ms)
         pred = rays / ((slow + g_ms) * 1e-3) / 1e6
         entry["splits"][n] = {
