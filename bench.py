@@ -462,14 +462,16 @@ def main():
     # it is the kernel's rate on the GPU
     busy_ms_step = busy_ms_all / world / args.steps
     alg_rate_busy = alg_bytes_all / world / args.steps / (busy_ms_step * 1e-3) / 1e9 if busy_ms_step > 0 else None
-    # PMC summaries of the headline workload measured by rocprofv3 on this build
-    # (tools/pmc_traffic.py, tools/pmc_valu.py; label = the build they were measured on).
-    # They describe the headline frame only, so they are never attached to another line.
-    headline = (args.scene is None and not args.primary_only and args.tris == 1_000_000 and args.res == 1024
-                and args.spp_sqrt == 10 and args.light_samples == 1 and args.emulate <= 1 and world == 1)
-    prof = os.path.join(ROOT, "profiles", PMC_PROFILE)
-    pmc_traffic = args.pmc_traffic or (prof + "_pmc_traffic.json" if headline else None)
-    pmc_valu = args.pmc_valu or (prof + "_pmc_valu.json" if headline else None)
+    # PMC summaries of this workload measured by rocprofv3 on this build (tools/pmc_traffic.py,
+    # tools/pmc_valu.py; label = the build they were measured on): the headline frame and C5
+    # (4096^2 x 64 spp, SURVEY.md 8(d)'s roofline config) each have their own, and a summary is
+    # never attached to another workload's line
+    soup = args.scene is None and not args.primary_only and args.tris == 1_000_000 and args.light_samples == 1
+    headline = soup and args.res == 1024 and args.spp_sqrt == 10 and args.emulate <= 1 and world == 1
+    c5 = soup and args.res == 4096 and args.spp_sqrt == 8 and args.emulate <= 1 and world == 1
+    prof = os.path.join(ROOT, "profiles", PMC_PROFILE + ("_c5" if c5 else ""))
+    pmc_traffic = args.pmc_traffic or (prof + "_pmc_traffic.json" if headline or c5 else None)
+    pmc_valu = args.pmc_valu or (prof + "_pmc_valu.json" if headline or c5 else None)
     traffic, traffic_src, pv = None, None, None
     if pmc_traffic and os.path.exists(pmc_traffic):
         pm = json.load(open(pmc_traffic))
@@ -518,9 +520,10 @@ def main():
                     "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None,
                     "alg_frac": round(alg_rate_busy / HBM_PEAK_GBS, 4) if alg_rate_busy else None,
                     "note": "the metric's '% HBM roofline': PMC HBM bytes (frac) and algorithmic bytes (alg_frac) "
-                            "per busy second vs 8 TB/s; the tree and primitives (~0.1 GB) are served from L2 / "
-                            "Infinity Cache, so HBM carries ~5 % of the algorithmic bytes and the kernel is bound "
-                            "by VALU issue instead (frac above)"},
+                            "per busy second vs 8 TB/s.  alg_frac above 1 is no HBM rate: the tree and primitives "
+                            "(~0.1 GB) are served from L2 / Infinity Cache, HBM carries a few % of the algorithmic "
+                            "bytes, and the north_star's HBM-read target does not apply at this working set; the "
+                            "binding roof is VALU issue (frac above)"},
             "l2": {"alg_bytes_per_launch": int(avg_launch_bytes), "alg_bytes_per_ray": round(bytes_per_ray, 1),
                    "model": "64 B per BVH4 node visit + prim_stride B per primitive test",
                    "achieved_gbs_per_launch": round(alg_rate, 1),

@@ -234,9 +234,11 @@ struct LogicArgs {
   const unsigned int* occl;
   unsigned int* wave_done;  // per slot-wave: 1 once all its slots retired (later steps skip it);
                             // kWaveIdle from logic_kernel to start_kernel: every slot is idle
-  // one-pass calls (camera_kernel -> one trace launch -> shade_reduce_kernel; slot == unit)
-  int op_kind;           // some tile reaches past the image: the query's kind word marks those units
-  int op_time;           // scenes with transformed shapes: the camera ray's time is stored (moving spheres)
+  // one-pass calls (camera_kernel -> one trace launch -> shade_reduce_kernel; slot == unit): the
+  // query record holds only what the call needs, field k of unit u at query[k * n_slots + u] --
+  // the direction in fields 0..2, then (-1: absent) the origin (thin lens), the ray time
+  // (transformed shapes: moving spheres) and a kind word (some tile reaches past the image)
+  int op_fo, op_ft, op_fk;
 };
 
 struct TraceArgs {
@@ -282,7 +284,7 @@ struct TraceArgs {
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
   int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
-  int op_kind, op_time;       // one-pass: read the kind word (units outside the image) / the ray time
+  int op_fo, op_ft, op_fk;    // one-pass query fields (LogicArgs): origin, time, kind; -1 absent
   float* help_hit;            // [n_threads][HIT_STRIDE]: a drain helper's closest-hit record
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
@@ -440,11 +442,14 @@ __device__ __forceinline__ void setup_query(Query& q, V3 o, V3 d, float tq, bool
 __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query& q) {
   if (a.one_pass) {  // the unit's camera ray (camera_kernel): 64-bit field offsets (up to 2^30 slots)
     const size_t n = (size_t)(unsigned)a.n_slots, u = (size_t)(unsigned)slot;
-    if (a.op_kind && __float_as_int(a.query[Q_KIND * n + u]) < 0) return false;
-    const V3 o = a.pinhole ? V3{a.cam_loc[0], a.cam_loc[1], a.cam_loc[2]}
-                           : V3{a.query[(Q_O + 0) * n + u], a.query[(Q_O + 1) * n + u], a.query[(Q_O + 2) * n + u]};
-    setup_query(q, o, V3{a.query[(Q_D + 0) * n + u], a.query[(Q_D + 1) * n + u], a.query[(Q_D + 2) * n + u]},
-                a.op_time ? a.query[Q_TMAX * n + u] : 0.0f, false);
+    if (a.op_fk >= 0 && __float_as_int(a.query[(size_t)a.op_fk * n + u]) < 0) return false;
+    V3 o{a.cam_loc[0], a.cam_loc[1], a.cam_loc[2]};
+    if (a.op_fo >= 0) {
+      const float* Qo = a.query + (size_t)a.op_fo * n + u;
+      o = V3{Qo[0], Qo[n], Qo[2 * n]};
+    }
+    setup_query(q, o, V3{a.query[u], a.query[n + u], a.query[2 * n + u]},
+                a.op_ft >= 0 ? a.query[(size_t)a.op_ft * n + u] : 0.0f, false);
     return true;
   }
   const int N = a.n_slots;
@@ -714,6 +719,93 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   return stack_pop_live(a, S, sp, gtid, lim);
 }
 
+#ifdef RT_COOP_LEAF
+// Cooperative leaf phase (planes-only instances; A/B build RT_COOP_LEAF).  A leaf phase runs
+// as many iterations as its largest waiting leaf has primitives, with the lanes whose leaves
+// are smaller idle (lane utilisation ~0.35).  Here the waiting leaves' (lane, primitive) pairs
+// are dealt over all 64 lanes through a per-wave byte table in LDS (the owner lane of pair
+// j), each pair lane tests its primitive against its owner's query (copied with ds_bpermute)
+// -- Plane::intersect, the exact reference-leaf filter -- and the hits, which are sparse, are
+// folded into their owners by a wave-uniform loop over readlane in lane order under the
+// (t, reference index) minimum (the result of any order: acceleration.cpp:112 first minimum),
+// any-hit queries by "occluded".  The pair lane whose hit ends its round as its owner's best
+// stores the owner's hit record.  Leaves have at most 4 primitives (the builder's SAH leaf),
+// so the table holds at most 256 pairs.
+constexpr int kCoopTabBytes = 256;  // per wave
+template <bool kCount>
+__device__ __forceinline__ void coop_leaf_planes(const TraceArgs& a, int slot, const Query& q, HitState& h, int item,
+                                                 int lane, uint64_t lane_lt, unsigned char* tab, unsigned int& nprim) {
+  const int cnt = is_leaf_item(item) ? (int)((uint32_t)item & 0x7fu) : 0;
+  int pre = 0, total = 0;  // exclusive prefix sum of cnt (< 8) over the wave, by bit slices
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const uint64_t m = __ballot((cnt >> b) & 1);
+    pre += __popcll(m & lane_lt) << b;
+    total += __popcll(m) << b;
+  }
+  for (int k = 0; k < cnt; ++k) tab[pre + k] = (unsigned char)lane;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const int qf = (int)q.par | (q.any ? 8 : 0);
+  for (int base = 0; base < total; base += 64) {
+    const int j = base + lane;
+    const int o = j < total ? (int)tab[j] : -1;
+    const int so = o >= 0 ? o : lane;
+    const int o_item = __shfl(item, so), o_pre = __shfl(pre, so);
+    Ray r;
+    r.o = V3{__shfl(q.r.o.x, so), __shfl(q.r.o.y, so), __shfl(q.r.o.z, so)};
+    r.d = V3{__shfl(q.r.d.x, so), __shfl(q.r.d.y, so), __shfl(q.r.d.z, so)};
+    r.time = 0.0f;
+    const float o_tmax = __shfl(q.tmax, so), o_bt = __shfl(h.best_t, so);
+    const int o_flags = __shfl(qf, so), o_br = __shfl(h.best_ref, so);
+    bool hit = false;
+    float t = 0.0f;
+    int ref = 0, pi = -1;
+    V3 X{0.0f, 0.0f, 0.0f}, nrm{0.0f, 0.0f, 0.0f};
+    uint32_t mat = 0;
+    if (o >= 0) {
+      pi = (int)(((uint32_t)o_item & ~kLeafBit) >> 7) + (j - o_pre);
+      PrimA P;
+      load_prim_a(a.c.prims + (size_t)pi * a.c.prim_stride4, P);
+      if (kCount) ++nprim;
+      if (plane_hit<false>(P, r, t, nullptr, &X)) {
+        const int2 rf = a.prim_refs[pi];
+        const bool better = (o_flags & 8) ? !(t > o_tmax) : (t < o_bt || (t == o_bt && rf.x < o_br));
+        if (better) {
+          hit = rf.y < 0 || plane_leaf_fast_ok(P, r, t, a.c.eps_abs) || ref_leaf_ok(a, rf.y, r, (uint32_t)(o_flags & 7));
+          ref = rf.x;
+          nrm = V3{P.a[3], P.a[7], P.a[11]};
+          mat = RT_TAG_MATERIAL(prim_tag(P));
+        }
+      }
+    }
+    uint64_t hm = __ballot(hit);
+    int win = -1;  // owner: the pair lane whose hit is its best after this round
+    while (hm != 0ull) {
+      const int hl = __ffsll((long long)hm) - 1;
+      hm &= hm - 1ull;
+      const int ow = __builtin_amdgcn_readlane(o, hl);
+      const float ht = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), hl));
+      const int hr = __builtin_amdgcn_readlane(ref, hl), hi = __builtin_amdgcn_readlane(pi, hl);
+      if (lane == ow) {
+        if (q.any) {
+          h.done = true;
+        } else if (ht < h.best_t || (ht == h.best_t && hr < h.best_ref)) {
+          h.best_t = ht;
+          h.best_ref = hr;
+          h.best_idx = hi;
+          win = hl;
+        }
+      }
+    }
+    if (!a.has_tex) {  // the winner stores the owner's record (test_prims' store, done by the pair lane)
+      const int w = __shfl(win, so), o_slot = __shfl(slot, so);
+      if (hit && w == lane && !(o_flags & 8)) store_hit_pnm(hit_rec(a.hit, o_slot), X, nrm, mat);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the table is rewritten by the next phase
+}
+#endif
+
 // Refill kernel.  Lanes that finished their query are handed new slots (from the wave's
 // current 64-slot range, then the next one) whenever fewer than `refill_min` lanes of the
 // wave still hold a query, so wave instructions keep most lanes busy instead of waiting for
@@ -785,6 +877,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
   int sp = 0;
   const LaneStack S{reinterpret_cast<int2*>(lds_stack) + threadIdx.x, reinterpret_cast<int2*>(a.spill)};
+#ifdef RT_COOP_LEAF
+  unsigned char* coop_tab = reinterpret_cast<unsigned char*>(lds_stack + (size_t)a.lds_entries * kBlock * 2) +
+                            (threadIdx.x >> 6) * kCoopTabBytes;
+#endif
   // a query was set up in q: start its traversal at the root (BVH::intersect_linear tests
   // every primitive at once, acceleration.cpp:124-139, and leaves nothing to traverse)
   auto start_traversal = [&]() {
@@ -983,6 +1079,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
     const uint64_t leafm = __ballot(is_leaf_item(item));
     if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+#ifdef RT_COOP_LEAF
+      if (kPlanesOnly) {
+        coop_leaf_planes<kCount>(a, slot, q, h, item, lane, lane_lt, coop_tab, nprim);
+        if (is_leaf_item(item)) {
+          lim = cull_limit(a, q, h);
+          item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
+        }
+      } else
+#endif
       if (is_leaf_item(item)) {
         const uint32_t e = (uint32_t)item;
         test_prims<kCount, kPlanesOnly>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
@@ -1635,7 +1740,8 @@ __device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, in
 // ops -- written to the query record of the slot with the unit's own index, and nothing else:
 // the direction; the origin for a thin-lens camera; the ray time for scenes with transformed
 // shapes (moving spheres; a plane ignores it, so planes-only scenes skip that draw); a kind
-// word only when some tile reaches past the image (those units: -1, and a miss result).
+// word only when some tile reaches past the image (those units: -1, and a miss result) -- in
+// the compact field layout of LogicArgs::op_fo / op_ft / op_fk.
 __global__ __launch_bounds__(kBlock) void camera_kernel(LogicArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.any_query = 1u;  // the trace launch runs
   const long long unit = (long long)blockIdx.x * kBlock + threadIdx.x;
@@ -1644,22 +1750,22 @@ __global__ __launch_bounds__(kBlock) void camera_kernel(LogicArgs a) {
   float* Q = a.query;
   int px, py, sample;
   if (!unit_coords(a, unit, px, py, sample)) {  // edge tile: pixel outside the image
-    Q[Q_KIND * N + u] = __int_as_float(-1);
+    Q[(size_t)a.op_fk * N + u] = __int_as_float(-1);
     a.result[u] = -1;
     return;
   }
   Rng rng;
   const Ray ray = sample_ray(a, px, py, sample, rng);
-  Q[(Q_D + 0) * N + u] = ray.d.x;
-  Q[(Q_D + 1) * N + u] = ray.d.y;
-  Q[(Q_D + 2) * N + u] = ray.d.z;
-  if (!a.pinhole) {
-    Q[(Q_O + 0) * N + u] = ray.o.x;
-    Q[(Q_O + 1) * N + u] = ray.o.y;
-    Q[(Q_O + 2) * N + u] = ray.o.z;
+  Q[u] = ray.d.x;
+  Q[N + u] = ray.d.y;
+  Q[2 * N + u] = ray.d.z;
+  if (a.op_fo >= 0) {
+    Q[(size_t)a.op_fo * N + u] = ray.o.x;
+    Q[(size_t)(a.op_fo + 1) * N + u] = ray.o.y;
+    Q[(size_t)(a.op_fo + 2) * N + u] = ray.o.z;
   }
-  if (a.op_time) Q[Q_TMAX * N + u] = (float)rng.next();
-  if (a.op_kind) Q[Q_KIND * N + u] = __int_as_float(a.pinhole ? kQueryCamOrigin : 0);
+  if (a.op_ft >= 0) Q[(size_t)a.op_ft * N + u] = (float)rng.next();
+  if (a.op_fk >= 0) Q[(size_t)a.op_fk * N + u] = __int_as_float(0);
 }
 
 // New samples.  A slot-wave whose 64 slots are all idle (every sample of its batch finished,
@@ -1845,9 +1951,11 @@ __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit, i
   V3 fin{base0.x * m.k_ambient, base0.y * m.k_ambient, base0.z * m.k_ambient};
   if (a.n_fuse > 0) {
     const size_t N = (size_t)(unsigned)a.n_slots;
-    const V3 ro = a.pinhole ? V3{a.cam.location[0], a.cam.location[1], a.cam.location[2]}
-                            : V3{a.query[(Q_O + 0) * N + unit], a.query[(Q_O + 1) * N + unit],
-                                 a.query[(Q_O + 2) * N + unit]};
+    V3 ro{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
+    if (a.op_fo >= 0) {
+      const float* Qo = a.query + (size_t)a.op_fo * N + unit;
+      ro = V3{Qo[0], Qo[N], Qo[2 * N]};
+    }
     for (int light = 0; light < a.n_lights; ++light) {
       const rt_light& L = a.lights[light];
       float vis = 0.0f;
@@ -2368,7 +2476,10 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     const bool planes = d->prim_stride == 64;
     auto occupancy = [&](const void* fn, bool six_waves) {
       const int lds_entries = std::min(d->stack_bound, lds_stack_entries(six_waves));
-      const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
+      size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
+#ifdef RT_COOP_LEAF
+      lds_bytes += (size_t)(kBlock / 64) * kCoopTabBytes;
+#endif
       int b = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, lds_bytes) != hipSuccess || b < 1) b = 2;
       if (const char* e = std::getenv("RT_TRACE_BPC")) b = std::max(1, std::min(b, std::atoi(e)));  // diagnostic
@@ -2558,10 +2669,21 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     HIP_TRY(hipMalloc(&s->d_tiles, (size_t)n_tiles * 2 * sizeof(int32_t)), RT_ENOMEM);
     s->tiles_cap = (size_t)n_tiles;
   }
+  // one-pass query record: the fields the call needs (LogicArgs::op_fo / op_ft / op_fk)
+  int op_fields = 3, op_fo = -1, op_ft = -1, op_fk = -1;
+  if (one_pass) {
+    if (cam->aperture > 0.0f) op_fo = op_fields, op_fields += 3;  // thin lens: the origin
+    if (!planes_only) op_ft = op_fields++;  // a plane ignores the ray time (a moving sphere needs it)
+    bool edge = false;  // some tile reaches past the image: its outside units are marked in a kind word
+    for (int i = 0; i < n_tiles && !edge; ++i)
+      edge = ((tile_ids[i] % tiles_x) + 1) * tile_w > cam->res_x || ((tile_ids[i] / tiles_x) + 1) * tile_h > cam->res_y;
+    if (edge) op_fk = op_fields++;
+  }
   {
     const size_t N = (size_t)std::max(n_slots, 1);
     int rc = RT_OK;
-    if ((rc = grow(s->d_query, s->cap_query, N * Q_COUNT * 4)) || (rc = grow(s->d_result, s->cap_result, N * 4)) ||
+    if ((rc = grow(s->d_query, s->cap_query, N * (one_pass ? op_fields : Q_COUNT) * 4)) ||
+        (rc = grow(s->d_result, s->cap_result, N * 4)) ||
         (rc = grow(s->d_hit, s->cap_hit, N * HIT_STRIDE * 4)) ||
         (tex_scene && (rc = grow(s->d_hit_uv, s->cap_hit_uv, N * sizeof(float2)))) ||
         (s->fuse_lights > 0 && (rc = grow(s->d_occl, s->cap_occl, N * 4))))
@@ -2712,14 +2834,12 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // the launched instance (launch_trace2): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
   // entries except fused shadows over transformed shapes (5, 16)
   ta.one_pass = one_pass ? 1 : 0;
-  ta.op_time = planes_only ? 0 : 1;  // a plane ignores the ray time (a moving sphere needs it)
-  la.op_time = ta.op_time;
-  {  // some tile reaches past the image: its outside units are marked in the kind word
-    bool edge = false;
-    for (int i = 0; i < n_tiles && !edge; ++i)
-      edge = ((tile_ids[i] % tiles_x) + 1) * tile_w > cam->res_x || ((tile_ids[i] / tiles_x) + 1) * tile_h > cam->res_y;
-    ta.op_kind = la.op_kind = edge ? 1 : 0;
-  }
+  ta.op_fo = op_fo;
+  ta.op_ft = op_ft;
+  ta.op_fk = op_fk;
+  la.op_fo = op_fo;
+  la.op_ft = op_ft;
+  la.op_fk = op_fk;
   const bool fuse_launch = ta.n_fuse > 0 || (one_pass && !planes_only), soft_launch = !fuse_launch && soft_trace;
   const bool six_waves = !(fuse_launch && !planes_only);
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(six_waves));
@@ -2728,7 +2848,10 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.occl = s->d_occl;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
   // entry + t_near per stack slot
-  const size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
+  size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
+#ifdef RT_COOP_LEAF
+  lds += (size_t)(kBlock / 64) * kCoopTabBytes;  // the cooperative leaf phase's pair tables
+#endif
 
   int replay_iter = -1, replay_reps = 0;
   const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
