@@ -179,8 +179,10 @@ def parse():
     ap.add_argument("--emulate", type=int, default=0,
                     help="diagnostic: render only rank --emulate-rank's tiles of an N-way split on this one GPU")
     ap.add_argument("--emulate-rank", type=int, default=0)
-    ap.add_argument("--deal", choices=["balanced", "lattice"], default="lattice",
-                    help="tiles -> ranks: equal counts balanced by the projected-centre cost estimate, or the 2-D lattice")
+    ap.add_argument("--deal", choices=["balanced", "measured", "lattice"], default="lattice",
+                    help="tiles -> ranks: the 2-D lattice; or equal counts balanced by a per-tile cost -- the "
+                         "projected-centre estimate (balanced), or the node visits of one instrumented render of the "
+                         "whole frame before timing (measured; rank 0 deals and broadcasts)")
     ap.add_argument("--light-radius", type=float, default=None,
                     help="override every light's radius (SURVEY.md 8(d) C4: soft shadows, e.g. 1.0)")
     ap.add_argument("--primary-only", action="store_true",
@@ -370,7 +372,23 @@ def main():
     # projected-centre cost estimate (every rank computes the same deal from the same scene;
     # its slowest rank measured slower than the lattice's)
     split = world if world > 1 else (args.emulate if args.emulate > 1 else 1)
-    deal = tl.balanced_deal(ds.tile_costs(T, T), split) if split > 1 and args.deal == "balanced" else None
+    deal = None
+    if split > 1 and args.deal == "balanced":
+        deal = tl.balanced_deal(ds.tile_costs(T, T), split)
+    elif split > 1 and args.deal == "measured":  # one instrumented render of the whole frame (not timed)
+        full = torch.empty(n_tiles * T * T * 3, dtype=torch.float32, device=f"cuda:{dev}")
+        ds.render_tiles(np.arange(n_tiles, dtype=np.int32), T, T, full.data_ptr(),
+                        rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True,
+                                        seed=args.seed, count_work=True))
+        del full
+        costs = ds.tile_costs_measured(T, T, args.spp_sqrt)
+        if (costs < 0).any():
+            raise SystemExit("bench.py --deal measured: the instrumented render measured no per-tile costs "
+                             "(the step pipeline does not; one-pass scenes only)")
+        deal_t = torch.as_tensor(tl.balanced_deal(costs, split), dtype=torch.int32, device=coll)
+        if dist:  # the measurement varies in its last bits between GPUs: rank 0's deal for everyone
+            dist.broadcast(deal_t, src=0)
+        deal = deal_t.cpu().numpy()
     mine = tl.assign_tiles(n_tiles, world, rank, tiles_x, deal)
     if args.emulate > 1 and world == 1:  # one rank's share of an N-way split (scaling prediction)
         mine = tl.assign_tiles(n_tiles, args.emulate, args.emulate_rank, tiles_x, deal)

@@ -225,6 +225,16 @@ int rt_render_tiles(rt_scene_t scene, const rt_camera_desc* cam, const rt_render
  * (Code/raytracer.cpp:433-476). */
 int rt_tile_costs(rt_scene_t scene, const rt_camera_desc* cam, int32_t tile_w, int32_t tile_h, float* costs_out);
 
+/* Measured per-tile cost: the BVH4 node visits the trace kernel made for each tile of the grid
+ * (tile id order) in the last instrumented (count_work) one-pass call of this camera, tile
+ * size and spp_sqrt -- -1 for tiles that call did not render (or when there was none).  The
+ * counts sum to that call's rt_stats.node_visits.  Multi-GPU callers deal tiles to ranks by
+ * it (bench.py --deal measured: one instrumented render of the whole frame, then
+ * tiles.balanced_deal); not deterministic in the last bits across runs (a wave's visits go to
+ * the tile it fetched last), so one rank computes the deal and broadcasts it. */
+int rt_tile_costs_measured(rt_scene_t scene, const rt_camera_desc* cam, int32_t tile_w, int32_t tile_h,
+                           int32_t spp_sqrt, float* costs_out);
+
 /* Small device-memory helpers so non-torch callers (ctypes tests, the C++ CLI) can drive
  * rt_render_tiles without their own HIP runtime bindings. */
 int rt_malloc(int32_t device, size_t bytes, void** d_ptr);

@@ -99,7 +99,7 @@ _host = None
 HIP_SYMBOLS = [
     "rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_tiles", "rt_malloc",
     "rt_free", "rt_memcpy_d2h", "rt_memcpy_h2d", "rt_synchronize", "rt_build_info", "rt_last_error",
-    "rt_quantise_device", "rt_tile_costs",
+    "rt_quantise_device", "rt_tile_costs", "rt_tile_costs_measured",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_free", "rth_scene_get_info", "rth_scene_desc", "rth_scene_camera",
@@ -139,6 +139,8 @@ def _load():
     _hip.rt_memcpy_h2d.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
     _hip.rt_quantise_device.argtypes = [c.c_void_p, c.c_int64, c.c_void_p, c.c_void_p]
     _hip.rt_tile_costs.argtypes = [c.c_void_p, c.POINTER(rt_camera_desc), c.c_int32, c.c_int32, c.POINTER(c.c_float)]
+    _hip.rt_tile_costs_measured.argtypes = [c.c_void_p, c.POINTER(rt_camera_desc), c.c_int32, c.c_int32, c.c_int32,
+                                            c.POINTER(c.c_float)]
     _hip.rt_synchronize.argtypes = [c.c_int32]
     _host.rth_last_error.restype = c.c_char_p
     _host.rth_scene_load.argtypes = [c.c_char_p, c.c_char_p, c.c_int32, c.c_int32, c.POINTER(c.c_void_p)]
@@ -323,6 +325,20 @@ class DeviceScene:
         out = np.zeros(tx * ty, dtype=np.float32)
         _check_hip(_hip.rt_tile_costs(self._h, ctypes.byref(self.cam), int(tile_w), int(tile_h),
                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), "rt_tile_costs")
+        return out
+
+
+    def tile_costs_measured(self, tile_w: int, tile_h: int, spp_sqrt: int) -> np.ndarray:
+        """rt_tile_costs_measured: BVH4 node visits per tile (tile id order) of the last
+        instrumented (count_work) one-pass render of this camera / tile size / spp; -1 where
+        that render did not cover the tile (or there was none)."""
+        if int(tile_w) <= 0 or int(tile_h) <= 0:
+            raise NativeError(f"rt_tile_costs_measured: tile size must be positive (got {tile_w}x{tile_h})")
+        tx = (self.cam.res_x + tile_w - 1) // tile_w
+        ty = (self.cam.res_y + tile_h - 1) // tile_h
+        out = np.zeros(tx * ty, dtype=np.float32)
+        _check_hip(_hip.rt_tile_costs_measured(self._h, ctypes.byref(self.cam), int(tile_w), int(tile_h), int(spp_sqrt),
+                                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), "rt_tile_costs_measured")
         return out
 
 

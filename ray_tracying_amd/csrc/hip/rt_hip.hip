@@ -285,6 +285,11 @@ struct TraceArgs {
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
   int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
   int op_fo, op_ft, op_fk;    // one-pass query fields (LogicArgs): origin, time, kind; -1 absent
+  // instrumented one-pass calls: node visits per render-order tile (unit / units per tile),
+  // summed per wave at each work fetch -- the measured cost later calls of this camera order
+  // their tiles by
+  unsigned int* tile_cost;
+  FastDiv fd_tile_units;
   float* help_hit;            // [n_threads][HIT_STRIDE]: a drain helper's closest-hit record
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
@@ -383,7 +388,7 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
   }
 }
 
-// cswap on non-negative (or +inf) floats compared as integers (RT_INT_CULL A/B build)
+// cswap on non-negative (or +inf) floats compared as integers (node_visit's child order)
 __device__ __forceinline__ void cswap_bits(float& ta, int& ca, float& tb, int& cb) {
   const int ia = __float_as_int(ta), ib = __float_as_int(tb);
   const bool sw = ib < ia;
@@ -391,15 +396,6 @@ __device__ __forceinline__ void cswap_bits(float& ta, int& ca, float& tb, int& c
   tb = __int_as_float(sw ? ia : ib);
   const int c = sw ? cb : ca;
   cb = sw ? ca : cb;
-  ca = c;
-}
-__device__ __forceinline__ void cswap(float& ta, int& ca, float& tb, int& cb) {
-  const bool sw = tb < ta;
-  const float t = sw ? tb : ta;
-  const int c = sw ? cb : ca;
-  tb = sw ? ta : tb;
-  cb = sw ? ca : cb;
-  ta = t;
   ca = c;
 }
 
@@ -529,6 +525,25 @@ __device__ __forceinline__ void trace_counters_out(const TraceArgs& ta, int lane
   }
 }
 
+// Instrumented (count_work) one-pass calls: the wave's node visits since its last work fetch
+// (its lanes' nvisit counts past their values then, `base`) added to the tile of the group it
+// fetched then -- most of the wave's rays come from it.  Production instances count nothing
+// (a per-visit count in the traversal loop cost 21 % through register pressure).
+__device__ __forceinline__ void flush_tile_cost(const TraceArgs& a, int lane, int tile, unsigned int nvisit,
+                                                unsigned int& base, unsigned int nrays, unsigned int& rbase) {
+  unsigned int v = nvisit - base, r = nrays - rbase;
+  base = nvisit;
+  rbase = nrays;
+  for (int off = 32; off > 0; off >>= 1) {
+    v += __shfl_xor(v, off);
+    r += __shfl_xor(r, off);
+  }
+  if (lane == 0 && tile >= 0 && (v | r)) {
+    atomicAdd(a.tile_cost + 2 * tile, v);
+    atomicAdd(a.tile_cost + 2 * tile + 1, r);
+  }
+}
+
 // ---- refill kernel with postponed leaves
 // Stack / item entries: a node index (>= 0), a leaf = kLeafBit | first << 7 | count (first <
 // 2^24, count < 128), or kNoItem.  Each stack entry carries its t_near so it is re-culled
@@ -652,8 +667,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   // t_near <= t_far, t_far >= 0 and t_near <= lim; misses sort last as (inf, entry)
   float t[4];
   int c[4];
-#ifdef RT_INT_CULL
-  // the same test on the values' bit patterns as signed integers (A/B build): for floats >= +0
+  // the test on the values' bit patterns as signed integers: for floats >= +0
   // integer order is float order, a negative float is a negative integer, so
   // max(tnx, tny, tnz, 0) is exact and a negative far distance still fails the test (its
   // value no longer matters); a far distance of exactly -0 now fails too -- conservative, as
@@ -666,36 +680,17 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     t[k] = __int_as_float(nb <= fb ? nb : 0x7f800000);
     c[k] = cc[k];
   }
-#else
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float n0 = fmaxf(fmaxf(tnx[k], tny[k]), fmaxf(tnz[k], 0.0f));
-    const float f0 = fminf(fminf(tfx[k], tfy[k]), fminf(tfz[k], lim));
-    t[k] = n0 <= f0 ? n0 : __builtin_inff();
-    c[k] = cc[k];
-  }
-#endif
   // Order the four (t, entry) pairs just enough: three compare-exchanges put the nearest
-  // first (the lane's next item), the pushes below need no order among the other three.  A
-  // full sort (5, RT_SORT_SWAPS A/B build) visits 0.7 % fewer nodes but costs 10 VALU more per
-  // visit: 4727 / 4736 vs 4797 / 4787 Mrays/s on one box (tools/exp_r02_47.sh).
-#ifndef RT_SORT_SWAPS
-#define RT_SORT_SWAPS 3
-#endif
-#ifdef RT_INT_CULL  // the t values are >= +0 or +inf: integer order on their bits
+  // first (the lane's next item), the pushes below need no order among the other three (a
+  // full sort, 5 exchanges, visits 0.7 % fewer nodes but was 1.3 % slower, round 2).  The t
+  // values are >= +0 or +inf: integer order on their bits (v_min/max_u32, no canonicalising
+  // of float operands).  r04 A/B of the integer cull + sort against the float one (same box,
+  // two boxes): headline +0.9 / +1.3 %, one rank's eighth +3.8 / +2.5 %, C3 +1.9 %, C2 -1.2 / -2.4 %.
   cswap_bits(t[0], c[0], t[1], c[1]);
   cswap_bits(t[2], c[2], t[3], c[3]);
   cswap_bits(t[0], c[0], t[2], c[2]);
   const bool v3 = __float_as_int(t[3]) != 0x7f800000, v2 = __float_as_int(t[2]) != 0x7f800000,
              v1 = __float_as_int(t[1]) != 0x7f800000;
-#else
-  cswap(t[0], c[0], t[1], c[1]);
-  cswap(t[2], c[2], t[3], c[3]);
-  cswap(t[0], c[0], t[2], c[2]);
-  if (RT_SORT_SWAPS >= 4) cswap(t[1], c[1], t[3], c[3]);
-  if (RT_SORT_SWAPS >= 5) cswap(t[1], c[1], t[2], c[2]);
-  const bool v3 = t[3] != __builtin_inff(), v2 = t[2] != __builtin_inff(), v1 = t[1] != __builtin_inff();
-#endif
   // push the three other children (entries 3, 2, 1; far-to-near when fully sorted).  Writes
   // at sp, sp+v3, sp+v3+v2 -- offsets counting only the children entered -- leave exactly
   // those below the new top whatever the order (a missed one lands on the next slot and is
@@ -711,100 +706,9 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     if (v2) stack_push(a, S, sp, gtid, c[2], t[2]);
     if (v1) stack_push(a, S, sp, gtid, c[1], t[1]);
   }
-#ifdef RT_INT_CULL
   if (__float_as_int(t[0]) != 0x7f800000) return c[0];
-#else
-  if (t[0] != __builtin_inff()) return c[0];
-#endif
   return stack_pop_live(a, S, sp, gtid, lim);
 }
-
-#ifdef RT_COOP_LEAF
-// Cooperative leaf phase (planes-only instances; A/B build RT_COOP_LEAF).  A leaf phase runs
-// as many iterations as its largest waiting leaf has primitives, with the lanes whose leaves
-// are smaller idle (lane utilisation ~0.35).  Here the waiting leaves' (lane, primitive) pairs
-// are dealt over all 64 lanes through a per-wave byte table in LDS (the owner lane of pair
-// j), each pair lane tests its primitive against its owner's query (copied with ds_bpermute)
-// -- Plane::intersect, the exact reference-leaf filter -- and the hits, which are sparse, are
-// folded into their owners by a wave-uniform loop over readlane in lane order under the
-// (t, reference index) minimum (the result of any order: acceleration.cpp:112 first minimum),
-// any-hit queries by "occluded".  The pair lane whose hit ends its round as its owner's best
-// stores the owner's hit record.  Leaves have at most 4 primitives (the builder's SAH leaf),
-// so the table holds at most 256 pairs.
-constexpr int kCoopTabBytes = 256;  // per wave
-template <bool kCount>
-__device__ __forceinline__ void coop_leaf_planes(const TraceArgs& a, int slot, const Query& q, HitState& h, int item,
-                                                 int lane, uint64_t lane_lt, unsigned char* tab, unsigned int& nprim) {
-  const int cnt = is_leaf_item(item) ? (int)((uint32_t)item & 0x7fu) : 0;
-  int pre = 0, total = 0;  // exclusive prefix sum of cnt (< 8) over the wave, by bit slices
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    const uint64_t m = __ballot((cnt >> b) & 1);
-    pre += __popcll(m & lane_lt) << b;
-    total += __popcll(m) << b;
-  }
-  for (int k = 0; k < cnt; ++k) tab[pre + k] = (unsigned char)lane;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  const int qf = (int)q.par | (q.any ? 8 : 0);
-  for (int base = 0; base < total; base += 64) {
-    const int j = base + lane;
-    const int o = j < total ? (int)tab[j] : -1;
-    const int so = o >= 0 ? o : lane;
-    const int o_item = __shfl(item, so), o_pre = __shfl(pre, so);
-    Ray r;
-    r.o = V3{__shfl(q.r.o.x, so), __shfl(q.r.o.y, so), __shfl(q.r.o.z, so)};
-    r.d = V3{__shfl(q.r.d.x, so), __shfl(q.r.d.y, so), __shfl(q.r.d.z, so)};
-    r.time = 0.0f;
-    const float o_tmax = __shfl(q.tmax, so), o_bt = __shfl(h.best_t, so);
-    const int o_flags = __shfl(qf, so), o_br = __shfl(h.best_ref, so);
-    bool hit = false;
-    float t = 0.0f;
-    int ref = 0, pi = -1;
-    V3 X{0.0f, 0.0f, 0.0f}, nrm{0.0f, 0.0f, 0.0f};
-    uint32_t mat = 0;
-    if (o >= 0) {
-      pi = (int)(((uint32_t)o_item & ~kLeafBit) >> 7) + (j - o_pre);
-      PrimA P;
-      load_prim_a(a.c.prims + (size_t)pi * a.c.prim_stride4, P);
-      if (kCount) ++nprim;
-      if (plane_hit<false>(P, r, t, nullptr, &X)) {
-        const int2 rf = a.prim_refs[pi];
-        const bool better = (o_flags & 8) ? !(t > o_tmax) : (t < o_bt || (t == o_bt && rf.x < o_br));
-        if (better) {
-          hit = rf.y < 0 || plane_leaf_fast_ok(P, r, t, a.c.eps_abs) || ref_leaf_ok(a, rf.y, r, (uint32_t)(o_flags & 7));
-          ref = rf.x;
-          nrm = V3{P.a[3], P.a[7], P.a[11]};
-          mat = RT_TAG_MATERIAL(prim_tag(P));
-        }
-      }
-    }
-    uint64_t hm = __ballot(hit);
-    int win = -1;  // owner: the pair lane whose hit is its best after this round
-    while (hm != 0ull) {
-      const int hl = __ffsll((long long)hm) - 1;
-      hm &= hm - 1ull;
-      const int ow = __builtin_amdgcn_readlane(o, hl);
-      const float ht = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), hl));
-      const int hr = __builtin_amdgcn_readlane(ref, hl), hi = __builtin_amdgcn_readlane(pi, hl);
-      if (lane == ow) {
-        if (q.any) {
-          h.done = true;
-        } else if (ht < h.best_t || (ht == h.best_t && hr < h.best_ref)) {
-          h.best_t = ht;
-          h.best_ref = hr;
-          h.best_idx = hi;
-          win = hl;
-        }
-      }
-    }
-    if (!a.has_tex) {  // the winner stores the owner's record (test_prims' store, done by the pair lane)
-      const int w = __shfl(win, so), o_slot = __shfl(slot, so);
-      if (hit && w == lane && !(o_flags & 8)) store_hit_pnm(hit_rec(a.hit, o_slot), X, nrm, mat);
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the table is rewritten by the next phase
-}
-#endif
 
 // Refill kernel.  Lanes that finished their query are handed new slots (from the wave's
 // current 64-slot range, then the next one) whenever fewer than `refill_min` lanes of the
@@ -856,6 +760,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   const int gtid = blockIdx.x * kBlock + threadIdx.x;
   unsigned int nbox = 0, nprim = 0, nvisit = 0;
   unsigned long long dg_any_rays = 0, dg_any_box = 0;
+  unsigned int nvc = 0, nrc = 0;  // count_work: nvisit / nrays at the wave's last work fetch (measured tile costs)
+  int cost_tile = -1;    // render-order tile of the wave's last fetched group
   const TraceArgs& a = ta;
   const unsigned int any = *ta.any_query;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ta.host_flag = any;  // read by the host after the step
@@ -877,10 +783,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
   int sp = 0;
   const LaneStack S{reinterpret_cast<int2*>(lds_stack) + threadIdx.x, reinterpret_cast<int2*>(a.spill)};
-#ifdef RT_COOP_LEAF
-  unsigned char* coop_tab = reinterpret_cast<unsigned char*>(lds_stack + (size_t)a.lds_entries * kBlock * 2) +
-                            (threadIdx.x >> 6) * kCoopTabBytes;
-#endif
   // a query was set up in q: start its traversal at the root (BVH::intersect_linear tests
   // every primitive at once, acceleration.cpp:124-139, and leaves nothing to traverse)
   auto start_traversal = [&]() {
@@ -1044,6 +946,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
               q_end = (unsigned)ta.slot_base + min(g * 64u + 64u, nq);
               // 64-slot groups are slot-waves of the logic step: skip one whose slots retired
               if (!a.one_pass && a.wave_done[q_next >> 6] != 0u) continue;
+              if (kCount && a.tile_cost) {  // the wave's node visits since its last fetch go to that group's tile
+                flush_tile_cost(a, lane, cost_tile, nvisit, nvc, nrays, nrc);
+                cost_tile = (int)fdiv(q_next, a.fd_tile_units);
+              }
               break;
             }
             if (++sk >= (int)nfs) {
@@ -1079,15 +985,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
     const uint64_t leafm = __ballot(is_leaf_item(item));
     if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
-#ifdef RT_COOP_LEAF
-      if (kPlanesOnly) {
-        coop_leaf_planes<kCount>(a, slot, q, h, item, lane, lane_lt, coop_tab, nprim);
-        if (is_leaf_item(item)) {
-          lim = cull_limit(a, q, h);
-          item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
-        }
-      } else
-#endif
       if (is_leaf_item(item)) {
         const uint32_t e = (uint32_t)item;
         test_prims<kCount, kPlanesOnly>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
@@ -1238,6 +1135,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     e[2] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+  if (kCount && a.tile_cost) flush_tile_cost(a, lane, cost_tile, nvisit, nvc, nrays, nrc);
   trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
 }
 
@@ -2084,9 +1982,13 @@ struct InitArgs {
   int fetch_words;
   unsigned int* batch_ctr;
   int batch_shards;
+  unsigned int* tile_cost;  // one-pass calls: the measured per-tile node visits, cleared
+  int n_tiles;
 };
 __global__ __launch_bounds__(kBlock) void init_kernel(InitArgs a) {
   for (int i = (int)threadIdx.x; i < a.ctl_words; i += kBlock) a.ctl[i] = 0u;
+  if (a.tile_cost)
+    for (int i = (int)threadIdx.x; i < a.n_tiles; i += kBlock) a.tile_cost[i] = 0u;
   for (int i = (int)threadIdx.x; i < a.fetch_words; i += kBlock) a.fetch[i] = 0u;
   const int waves = a.n_slots >> 6;
   for (int k = (int)threadIdx.x; k < a.batch_shards; k += kBlock)
@@ -2239,6 +2141,15 @@ struct rt_scene_s {
   std::vector<float> cost_pts;
   std::vector<unsigned char> cost_key;
   std::vector<float> tile_cost;
+  // measured tile costs (one-pass calls): lane node visits per tile id of the last calls with
+  // this camera / tile size / sample count (-1: not measured yet), and their device / pinned
+  // host counters
+  std::vector<unsigned char> meas_key;
+  std::vector<float> meas_cost;    // the order key: node visits per ray of the tile (RT_MEASURED_ORDER=2: total)
+  std::vector<float> meas_visits;  // node visits of the tile
+  unsigned int* d_tile_cost = nullptr;
+  unsigned int* h_tile_cost = nullptr;
+  size_t cap_tile_cost = 0, cap_h_tile_cost = 0;
   int fuse_lights = 0;  // > 0: point lights whose shadow rays the trace kernel may fuse (see rt_scene_create)
 };
 
@@ -2302,12 +2213,36 @@ static const std::vector<float>& tile_costs(rt_scene_s* s, const rt_camera_desc*
   return s->tile_cost;
 }
 
+// The key of measured tile costs: camera, tile size, samples per pixel.
+static std::vector<unsigned char> meas_key_of(const rt_camera_desc* cam, int tile_w, int tile_h, int n_samples) {
+  std::vector<unsigned char> key(sizeof(rt_camera_desc) + 3 * sizeof(int));
+  std::memcpy(key.data(), cam, sizeof(rt_camera_desc));
+  const int v[3] = {tile_w, tile_h, n_samples};
+  std::memcpy(key.data() + sizeof(rt_camera_desc), v, sizeof(v));
+  return key;
+}
+
+// Tiles with a measured cost (an earlier instrumented one-pass call -- count_work -- of this
+// camera / tile size / sample count: its trace kernel's node visits per tile) are ordered by it -- it sees what the
+// projected-centre estimate misses, the rays that graze the object's silhouette and cross
+// much of it; the others by the estimate.
 static void tile_cost_order(rt_scene_s* s, const rt_camera_desc* cam, int tile_w, int tile_h, int tiles_x, int tiles_y,
-                            const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
+                            int n_samples, const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
   order.resize((size_t)n_tiles);
   for (int i = 0; i < n_tiles; ++i) order[i] = i;
   if (const char* e = std::getenv("RT_TILE_ORDER")) wanted = std::atoi(e) != 0;  // 0 / 1: never / always
-  if (!wanted || n_tiles < 2 || s->cost_pts.empty()) return;
+  if (!wanted || n_tiles < 2) return;
+  bool measured = false;  // RT_MEASURED_ORDER=1 / 2: by measured cost per ray / total (A/B; the estimate by default)
+  if (const char* e = std::getenv("RT_MEASURED_ORDER"))
+    measured = std::atoi(e) != 0 && s->meas_key == meas_key_of(cam, tile_w, tile_h, n_samples);
+  for (int i = 0; i < n_tiles && measured; ++i) measured = s->meas_cost[(size_t)tile_ids[i]] >= 0.0f;
+  if (measured) {
+    std::stable_sort(order.begin(), order.end(), [&](int i, int j) {
+      return s->meas_cost[(size_t)tile_ids[i]] > s->meas_cost[(size_t)tile_ids[j]];
+    });
+    return;
+  }
+  if (s->cost_pts.empty()) return;
   const std::vector<float>& cost = tile_costs(s, cam, tile_w, tile_h, tiles_x, tiles_y);
   std::stable_sort(order.begin(), order.end(), [&](int i, int j) {
     return cost[(size_t)tile_ids[i]] > cost[(size_t)tile_ids[j]];
@@ -2366,6 +2301,8 @@ int rt_scene_destroy(rt_scene_t s) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
+  if (s->d_tile_cost) (void)hipFree(s->d_tile_cost);
+  if (s->h_tile_cost) (void)hipHostFree(s->h_tile_cost);
   if (s->h_stats) (void)hipHostFree(s->h_stats);
   hipEvent_t evs[] = {s->ev_t0, s->ev_t1, s->ev_fork, s->ev_join};
   for (hipEvent_t e : evs)
@@ -2476,10 +2413,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     const bool planes = d->prim_stride == 64;
     auto occupancy = [&](const void* fn, bool six_waves) {
       const int lds_entries = std::min(d->stack_bound, lds_stack_entries(six_waves));
-      size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
-#ifdef RT_COOP_LEAF
-      lds_bytes += (size_t)(kBlock / 64) * kCoopTabBytes;
-#endif
+      const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
       int b = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, lds_bytes) != hipSuccess || b < 1) b = 2;
       if (const char* e = std::getenv("RT_TRACE_BPC")) b = std::max(1, std::min(b, std::atoi(e)));  // diagnostic
@@ -2582,6 +2516,18 @@ static long long one_pass_cap() {
 }
 
 extern "C" {
+
+int rt_tile_costs_measured(rt_scene_t s, const rt_camera_desc* cam, int32_t tile_w, int32_t tile_h, int32_t spp_sqrt,
+                           float* costs_out) {
+  if (!s || !cam || !costs_out) return fail(RT_EINVAL, "rt_tile_costs_measured: null argument");
+  if (tile_w <= 0 || tile_h <= 0) return fail(RT_EINVAL, "rt_tile_costs_measured: tile size must be positive");
+  if (cam->res_x <= 0 || cam->res_y <= 0) return fail(RT_EINVAL, "rt_tile_costs_measured: camera resolution is 0");
+  const int tiles_x = (cam->res_x + tile_w - 1) / tile_w, tiles_y = (cam->res_y + tile_h - 1) / tile_h;
+  const int n_samples = spp_sqrt <= 1 ? 1 : spp_sqrt * spp_sqrt;
+  const bool have = s->meas_key == meas_key_of(cam, tile_w, tile_h, n_samples);
+  for (int i = 0; i < tiles_x * tiles_y; ++i) costs_out[i] = have ? s->meas_visits[(size_t)i] : -1.0f;
+  return RT_OK;
+}
 
 int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
                     int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
@@ -2704,7 +2650,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // 4509-4564 -> 4723-4727 Mrays/s.  Longer calls keep the caller's order (whole frames,
   // C4, C5: within -1.6 %..+0 % -- the other pipeline hides their drains).
   std::vector<int32_t> order;
-  tile_cost_order(s, cam, tile_w, tile_h, tiles_x, tiles_y, tile_ids, n_tiles, n_units <= n_slots, order);
+  tile_cost_order(s, cam, tile_w, tile_h, tiles_x, tiles_y, n_samples, tile_ids, n_tiles, n_units <= n_slots, order);
   std::vector<int32_t> tl_dev((size_t)n_tiles * 2);
   bool identity = true;
   for (int i = 0; i < n_tiles; ++i) {
@@ -2834,6 +2780,20 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // the launched instance (launch_trace2): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
   // entries except fused shadows over transformed shapes (5, 16)
   ta.one_pass = one_pass ? 1 : 0;
+  ta.tile_cost = nullptr;
+  const bool measure_tiles = one_pass && p->count_work;
+  if (measure_tiles) {  // the per-tile node visits later calls of this camera order their tiles by
+    if (const int rc = grow(s->d_tile_cost, s->cap_tile_cost, (size_t)n_tiles * 8)) return rc;
+    if ((size_t)n_tiles * 8 > s->cap_h_tile_cost) {
+      if (s->h_tile_cost) (void)hipHostFree(s->h_tile_cost);
+      s->h_tile_cost = nullptr;
+      s->cap_h_tile_cost = 0;
+      HIP_TRY(hipHostMalloc((void**)&s->h_tile_cost, (size_t)n_tiles * 8), RT_ENOMEM);
+      s->cap_h_tile_cost = (size_t)n_tiles * 8;
+    }
+    ta.tile_cost = s->d_tile_cost;
+    ta.fd_tile_units = make_fastdiv((uint32_t)(tile_w * tile_h * n_samples));
+  }
   ta.op_fo = op_fo;
   ta.op_ft = op_ft;
   ta.op_fk = op_fk;
@@ -2848,10 +2808,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   la.occl = s->d_occl;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
   // entry + t_near per stack slot
-  size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
-#ifdef RT_COOP_LEAF
-  lds += (size_t)(kBlock / 64) * kCoopTabBytes;  // the cooperative leaf phase's pair tables
-#endif
+  const size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
 
   int replay_iter = -1, replay_reps = 0;
   const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
@@ -2943,6 +2900,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     ia.fetch_words = (int)(kPipes * kFetchLines * kFetchStride);
     ia.batch_ctr = s->d_batch_ctr;
     ia.batch_shards = la.batch_shards;
+    ia.tile_cost = pipes[0].ta.tile_cost;
+    ia.n_tiles = 2 * n_tiles;
     hipLaunchKernelGGL(init_kernel, dim3(1), dim3(kBlock), 0, stream, ia);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
   }
@@ -2997,8 +2956,27 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     else hipLaunchKernelGGL(shade_reduce_kernel<false>, dim3(rblocks), dim3(kBlock), 0, stream, la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     if (stats) HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    if (measure_tiles)
+      HIP_TRY(hipMemcpyAsync(s->h_tile_cost, s->d_tile_cost, (size_t)n_tiles * 8, hipMemcpyDeviceToHost, stream),
+              RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
     HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
+    if (measure_tiles) {  // measured tile costs, by tile id (render-order index i holds tile tl_dev[i])
+      const std::vector<unsigned char> key = meas_key_of(cam, tile_w, tile_h, n_samples);
+      if (s->meas_key != key) {
+        s->meas_key = key;
+        s->meas_cost.assign((size_t)tiles_x * tiles_y, -1.0f);
+        s->meas_visits.assign((size_t)tiles_x * tiles_y, -1.0f);
+      }
+      // RT_MEASURED_ORDER=2: total node visits; default: node visits per ray (a tile's mean
+      // ray cost -- where the long rays are)
+      const bool total = std::getenv("RT_MEASURED_ORDER") && std::atoi(std::getenv("RT_MEASURED_ORDER")) == 2;
+      for (int i = 0; i < n_tiles; ++i) {
+        const float v = (float)s->h_tile_cost[2 * i], r = (float)s->h_tile_cost[2 * i + 1];
+        s->meas_cost[(size_t)tl_dev[i]] = total ? v : (r > 0.0f ? v / r : 0.0f);
+        s->meas_visits[(size_t)tl_dev[i]] = v;
+      }
+    }
     float ms = 0.f, t_a = 0.f, t_b = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[0][0], s->ev_b[0][0]), RT_EDEVICE);
     if (stats && hipEventElapsedTime(&t_a, s->ev_t0, s->ev_a[0][0]) == hipSuccess &&

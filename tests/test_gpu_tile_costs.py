@@ -71,3 +71,31 @@ def test_tile_costs_match_camera_rays(tmp_path, gpu):
             ds.close()
     finally:
         sc.close()
+
+
+def test_measured_tile_costs_sum_to_node_visits(tmp_path, gpu):
+    """rt_tile_costs_measured: an instrumented (count_work) one-pass render leaves each tile's
+    BVH4 node visits; over a whole frame they sum to the call's node_visits, and a tile left
+    out of the call reads -1.  Before any instrumented call every tile reads -1."""
+    import torch
+    sc = rt.Scene(scenes.write(scenes.soup(3000, seed=4, res=(192, 128)), str(tmp_path / "s.json")))
+    ds = rt.DeviceScene(sc, 0)
+    try:
+        T = 32
+        n = (192 // T) * (128 // T)
+        assert (ds.tile_costs_measured(T, T, 2) == -1).all()
+        buf = torch.zeros(n * T * T * 3, dtype=torch.float32, device="cuda:0")
+        ids = np.arange(n, dtype=np.int32)
+        p = rt.RenderParams(spp_sqrt=2, light_samples=1, use_bvh=True, seed=3, count_work=True)
+        st = ds.render_tiles(ids[1:], T, T, buf.data_ptr(), p)  # every tile but tile 0
+        assert st.path == rt.PATH_ONE_PASS
+        m = ds.tile_costs_measured(T, T, 2)
+        assert m[0] == -1 and (m[1:] >= 0).all()
+        assert int(m[1:].sum()) == st.node_visits and st.node_visits > 0
+        assert (ds.tile_costs_measured(T, T, 3) == -1).all()  # another sample count: not measured
+        st = ds.render_tiles(ids, T, T, buf.data_ptr(), p)
+        m = ds.tile_costs_measured(T, T, 2)
+        assert (m >= 0).all() and int(m.sum()) == st.node_visits
+    finally:
+        ds.close()
+        sc.close()
