@@ -200,6 +200,9 @@ def parse():
     ap.add_argument("--ubench", default=None,
                     help="JSON of the counter-measured VALU microbenchmark (tools/pmc_ubench.py): the measured VALU "
                          "peak; default: the committed profile")
+    ap.add_argument("--frames-in-flight", type=int, default=1,
+                    help="frames rendered concurrently (scene handles on their own streams; one-pass scenes): the next "
+                         "frame's camera rays and the previous frame's shading fill the tail of the other's trace launch")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")
     return ap.parse_args()
@@ -408,6 +411,43 @@ def main():
             gathered = tl.gather_to_root(dist, out if coll != "cpu" else out.cpu(), rank, world)
         return st
 
+    # Frames in flight (--frames-in-flight F > 1): frame k renders on scene handle k % F and its
+    # own HIP stream, deferred (RenderParams.sync=False), and is finished -- waited for, its
+    # framebuffer gathered -- only once frame k + F - 1 is enqueued, so the next frame's camera
+    # rays and this frame's shading run in the idle tail of the other frame's trace launch.
+    # Every frame is rendered in full and gathered; steps are timed exactly as with F = 1.
+    F = max(1, args.frames_in_flight)
+    fl_ds = [ds] + [rt.DeviceScene(scene, dev) for _ in range(F - 1)]
+    fl_out = [out] + [torch.zeros_like(out) for _ in range(F - 1)]
+    fl_st = [torch.cuda.Stream(device=dev) for _ in range(F)] if F > 1 else []
+
+    def issue(k, seed):
+        i = k % F
+        p = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=seed,
+                            sync=False)
+        fl_ds[i].render_tiles(mine, T, T, fl_out[i].data_ptr(), p, stream=fl_st[i].cuda_stream)
+
+    def finish(k):
+        nonlocal gathered
+        i = k % F
+        st = fl_ds[i].wait()
+        if dist:  # the frame is complete (wait): gather it to rank 0 over RCCL / xGMI
+            gathered = tl.gather_to_root(dist, fl_out[i] if coll != "cpu" else fl_out[i].cpu(), rank, world)
+        return st
+
+    def run_frames(seeds):
+        """Render the frames (F in flight) and return their stats in order."""
+        if F == 1:
+            return [step(sd) for sd in seeds]
+        sts = []
+        for k, sd in enumerate(seeds):
+            issue(k, sd)
+            if k >= F - 1:
+                sts.append(finish(k - F + 1))
+        for k in range(max(0, len(seeds) - F + 1), len(seeds)):
+            sts.append(finish(k))
+        return sts
+
     # ---- instrumented frame: algorithmic bytes per ray (same seed as the first timed step)
     cp = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=args.seed,
                          count_work=True)
@@ -419,8 +459,7 @@ def main():
         f"({cst.box_tests / max(cst.rays, 1):.1f}/ray), prim tests {cst.prim_tests} "
         f"({cst.prim_tests / max(cst.rays, 1):.2f}/ray), {bytes_per_ray:.0f} B/ray")
 
-    for w in range(args.warmup):
-        step(args.seed + 1000 + w)
+    run_frames([args.seed + 1000 + w for w in range(args.warmup)])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -431,8 +470,7 @@ def main():
     busy_ms = 0.0
     launches = 0
     one_pass = True
-    for k in range(args.steps):
-        st = step(args.seed + k)
+    for st in run_frames([args.seed + k for k in range(args.steps)]):
         one_pass = one_pass and st.path == rt.PATH_ONE_PASS
         rays += st.rays
         trace_ms += st.trace_ms
@@ -571,6 +609,7 @@ def main():
             "resolution": f"{W}x{H}", "spp": max(1, args.spp_sqrt) ** 2, "flags": f"-bvh -s {args.spp_sqrt} -light_sample {args.light_samples}",
             "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}" + (f" ({args.deal} deal)" if split > 1 else ""),
             "rng": "counter (splitmix64 per pixel/sample)",
+            "frames_in_flight": F,
             "pipeline": ("one-pass (camera_kernel -> one trace_refill_kernel launch -> shade_reduce_kernel)" if one_pass
                          else "steps (logic -> start -> trace over slot state, then reduce)"),
             **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),

@@ -173,7 +173,9 @@ typedef struct rt_render_params {
   int32_t use_bvh;       /* -bvh (0: linear search over all primitives, acceleration.cpp:124) */
   int32_t count_work;    /* 1: instrumented kernel, fills box_tests / prim_tests */
   uint64_t seed;         /* counter-RNG seed */
-  int32_t sync;          /* 1: synchronise and fill kernel_ms before returning */
+  int32_t sync;          /* 1: wait for the render and fill the stats before returning; 0: a one-pass
+                            call (rt_stats.path) returns once enqueued on `stream` -- rt_render_wait
+                            (or the scene's next call) finishes it; step-pipeline calls always wait */
   int32_t pad;
 } rt_render_params;
 
@@ -215,6 +217,13 @@ int rt_scene_destroy(rt_scene_t scene);
 int rt_render_tiles(rt_scene_t scene, const rt_camera_desc* cam, const rt_render_params* params,
                     const int32_t* tile_ids, int32_t n_tiles, int32_t tile_w, int32_t tile_h,
                     float* d_rgb_out, void* stream, rt_stats* stats);
+
+/* Finishes the scene's deferred call (rt_render_params.sync == 0): waits for it and fills
+ * `stats` (may be null); with nothing deferred it returns zeroed stats.  Two scene handles of
+ * one scene on two streams keep two frames in flight (bench.py --frames-in-flight 2): the
+ * next frame's camera rays and the previous frame's shading run in the idle tail of the
+ * other frame's trace launch. */
+int rt_render_wait(rt_scene_t scene, rt_stats* stats);
 
 /* Per-tile cost estimate of a frame (host only, no device work): for every tile of the
  * ceil(res_x/tile_w) x ceil(res_y/tile_h) grid (tile id order), how many of a sample of up to

@@ -99,7 +99,7 @@ _host = None
 HIP_SYMBOLS = [
     "rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_tiles", "rt_malloc",
     "rt_free", "rt_memcpy_d2h", "rt_memcpy_h2d", "rt_synchronize", "rt_build_info", "rt_last_error",
-    "rt_quantise_device", "rt_tile_costs", "rt_tile_costs_measured",
+    "rt_quantise_device", "rt_tile_costs", "rt_tile_costs_measured", "rt_render_wait",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_free", "rth_scene_get_info", "rth_scene_desc", "rth_scene_camera",
@@ -141,6 +141,7 @@ def _load():
     _hip.rt_tile_costs.argtypes = [c.c_void_p, c.POINTER(rt_camera_desc), c.c_int32, c.c_int32, c.POINTER(c.c_float)]
     _hip.rt_tile_costs_measured.argtypes = [c.c_void_p, c.POINTER(rt_camera_desc), c.c_int32, c.c_int32, c.c_int32,
                                             c.POINTER(c.c_float)]
+    _hip.rt_render_wait.argtypes = [c.c_void_p, c.POINTER(rt_stats)]
     _hip.rt_synchronize.argtypes = [c.c_int32]
     _host.rth_last_error.restype = c.c_char_p
     _host.rth_scene_load.argtypes = [c.c_char_p, c.c_char_p, c.c_int32, c.c_int32, c.POINTER(c.c_void_p)]
@@ -201,10 +202,11 @@ class RenderParams:
     use_bvh: bool = True       # -bvh
     seed: int = 20251226
     count_work: bool = False   # instrumented run: fill box_tests / prim_tests
+    sync: bool = True          # False: a one-pass call returns once enqueued (DeviceScene.wait finishes it)
 
     def c(self) -> rt_render_params:
         return rt_render_params(int(self.spp_sqrt), int(self.light_samples), 1 if self.use_bvh else 0,
-                                1 if self.count_work else 0, int(self.seed) & (2**64 - 1), 1, 0)
+                                1 if self.count_work else 0, int(self.seed) & (2**64 - 1), 1 if self.sync else 0, 0)
 
 
 PATH_STEPS, PATH_ONE_PASS = 0, 1  # rt_stats.path (include/rt_hip.h)
@@ -327,6 +329,13 @@ class DeviceScene:
                                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))), "rt_tile_costs")
         return out
 
+
+    def wait(self) -> RenderStats:
+        """rt_render_wait: finish this scene's deferred call (RenderParams(sync=False)) and return
+        its statistics (zeros when nothing is deferred)."""
+        st = rt_stats()
+        _check_hip(_hip.rt_render_wait(self._h, ctypes.byref(st)), "rt_render_wait")
+        return RenderStats.of(st)
 
     def tile_costs_measured(self, tile_w: int, tile_h: int, spp_sqrt: int) -> np.ndarray:
         """rt_tile_costs_measured: BVH4 node visits per tile (tile id order) of the last

@@ -283,6 +283,7 @@ struct TraceArgs {
   int frames, pinhole;
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
+  int drain_leaf_div;         // drain loop: leaf phase once 1/drain_leaf_div of the active lanes wait (0: off)
   int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
   int op_fo, op_ft, op_fk;    // one-pass query fields (LogicArgs): origin, time, kind; -1 absent
   // instrumented one-pass calls: node visits per render-order tile (unit / units per tile),
@@ -1114,7 +1115,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       }
       const uint64_t act = __ballot(item != kNoItem);
       const uint64_t leafm = __ballot(is_leaf_item(item));
-      if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+      // the tail is latency-bound: with few lanes left a leaf is tested once 1/drain_leaf_div of
+      // them wait on one, not only when leaf_min do (or nothing else is left)
+      const int nleaf = __popcll(leafm);
+      if (leafm != 0ull && (nleaf >= a.leaf_min || (act & ~leafm) == 0ull ||
+                            (a.drain_leaf_div > 0 && nleaf * a.drain_leaf_div >= __popcll(act)))) {
         if (is_leaf_item(item)) {
           const uint32_t e = (uint32_t)item;
           test_prims<kCount, kPlanesOnly, true>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax,
@@ -2150,6 +2155,17 @@ struct rt_scene_s {
   unsigned int* d_tile_cost = nullptr;
   unsigned int* h_tile_cost = nullptr;
   size_t cap_tile_cost = 0, cap_h_tile_cost = 0;
+  // a deferred one-pass call (rt_render_params.sync == 0): enqueued, not yet waited for --
+  // what rt_render_wait (or the scene's next call) needs to finish it
+  struct Pending {
+    bool active = false, count_work = false, measure_tiles = false;
+    int n_tiles = 0, tiles_x = 0, tiles_y = 0;
+    std::vector<int32_t> tl_dev;
+    std::vector<unsigned char> meas_key;
+#ifdef RT_EXIT_TIMING
+    TraceArgs ta{};
+#endif
+  } pending;
   int fuse_lights = 0;  // > 0: point lights whose shadow rays the trace kernel may fuse (see rt_scene_create)
 };
 
@@ -2489,6 +2505,55 @@ static int print_exit_log(const TraceArgs& ta, float ms, int step) {
 }
 #endif
 
+// Finishes the scene's enqueued one-pass call: waits for its last event, records its measured
+// tile costs (instrumented calls) and fills `stats` (may be null).
+static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
+  rt_scene_s::Pending& q = s->pending;
+  if (!q.active) {
+    if (stats) *stats = rt_stats{};
+    return RT_OK;
+  }
+  q.active = false;
+  HIP_TRY(hipSetDevice(s->device), RT_EDEVICE);
+  HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
+  if (q.measure_tiles) {  // measured tile costs, by tile id (render-order index i holds tile tl_dev[i])
+    if (s->meas_key != q.meas_key) {
+      s->meas_key = q.meas_key;
+      s->meas_cost.assign((size_t)q.tiles_x * q.tiles_y, -1.0f);
+      s->meas_visits.assign((size_t)q.tiles_x * q.tiles_y, -1.0f);
+    }
+    // RT_MEASURED_ORDER=2: total node visits; otherwise node visits per ray (a tile's mean ray cost)
+    const bool total = std::getenv("RT_MEASURED_ORDER") && std::atoi(std::getenv("RT_MEASURED_ORDER")) == 2;
+    for (int i = 0; i < q.n_tiles; ++i) {
+      const float v = (float)s->h_tile_cost[2 * i], r = (float)s->h_tile_cost[2 * i + 1];
+      s->meas_cost[(size_t)q.tl_dev[i]] = total ? v : (r > 0.0f ? v / r : 0.0f);
+      s->meas_visits[(size_t)q.tl_dev[i]] = v;
+    }
+  }
+  float ms = 0.f, t_a = 0.f, t_b = 0.f, k_ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[0][0], s->ev_b[0][0]), RT_EDEVICE);
+#ifdef RT_EXIT_TIMING
+  if (const int rc = print_exit_log(q.ta, ms, 0)) return rc;
+#endif
+  s->last_iters = 1;
+  if (!stats) return RT_OK;
+  *stats = rt_stats{};
+  const unsigned long long* h = s->h_stats;
+  HIP_TRY(hipEventElapsedTime(&k_ms, s->ev_t0, s->ev_t1), RT_EDEVICE);
+  HIP_TRY(hipEventElapsedTime(&t_a, s->ev_t0, s->ev_a[0][0]), RT_EDEVICE);
+  HIP_TRY(hipEventElapsedTime(&t_b, s->ev_t0, s->ev_b[0][0]), RT_EDEVICE);
+  stats->rays = h[4];  // ctl bytes 16, 24, 32: box tests, prim tests, rays
+  stats->box_tests = h[2];
+  stats->prim_tests = h[3];
+  stats->kernel_ms = k_ms;
+  stats->trace_ms = ms;
+  stats->trace_busy_ms = t_b - t_a;
+  stats->iterations = 1;
+  stats->path = RT_PATH_ONE_PASS;
+  stats->node_visits = q.count_work ? h[61] : 0;
+  return RT_OK;
+}
+
 // One-pass calls: camera_kernel -> one trace launch -> shade_reduce_kernel, slot == unit and no
 // slot state.  The scene must need nothing between a sample's camera ray and its colour but the
 // closest hit and one shadow ray per light, traced by the tracing lane: no Trace recursion
@@ -2517,6 +2582,11 @@ static long long one_pass_cap() {
 
 extern "C" {
 
+int rt_render_wait(rt_scene_t s, rt_stats* stats) {
+  if (!s) return fail(RT_EINVAL, "rt_render_wait: null scene");
+  return finish_one_pass(s, stats);
+}
+
 int rt_tile_costs_measured(rt_scene_t s, const rt_camera_desc* cam, int32_t tile_w, int32_t tile_h, int32_t spp_sqrt,
                            float* costs_out) {
   if (!s || !cam || !costs_out) return fail(RT_EINVAL, "rt_tile_costs_measured: null argument");
@@ -2541,6 +2611,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const int tiles_x = (cam->res_x + tile_w - 1) / tile_w, tiles_y = (cam->res_y + tile_h - 1) / tile_h;
   for (int i = 0; i < n_tiles; ++i)
     if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y) return fail(RT_EINVAL, "rt_render_tiles: tile id out of range");
+  if (s->pending.active)  // the scene's deferred call finishes first (its workspace is reused)
+    if (const int rc = finish_one_pass(s, nullptr)) return rc;
   if (stats) *stats = rt_stats{};
   if (n_tiles == 0) return RT_OK;
   {  // calls larger than the unit cap run as consecutive tile chunks (same pixels: the counter
@@ -2554,9 +2626,11 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       const int k = (int)std::max(1LL, std::min<long long>(n_tiles, cap / per_tile));
       rt_stats acc{};
       acc.path = RT_PATH_ONE_PASS;
+      rt_render_params pc = *p;
+      pc.sync = 1;  // chunks share the workspace: each one finishes before the next
       for (int t0 = 0; t0 < n_tiles; t0 += k) {
         rt_stats st{};
-        const int rc = rt_render_tiles(s, cam, p, tile_ids + t0, std::min(k, n_tiles - t0), tile_w, tile_h,
+        const int rc = rt_render_tiles(s, cam, &pc, tile_ids + t0, std::min(k, n_tiles - t0), tile_w, tile_h,
                                        d_out + (size_t)t0 * tile_w * tile_h * 3, stream_ptr, &st);
         if (rc) return rc;
         acc.rays += st.rays;
@@ -2759,6 +2833,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // are the serial near-first traversal's (the algorithmic bytes bench.py reports)
   ta.drain_help = p->count_work ? 0 : 1;
   if (const char* e = std::getenv("RT_DRAIN_HELP")) ta.drain_help = std::atoi(e) != 0 ? 1 : 0;
+  ta.drain_leaf_div = 0;
+  if (const char* e = std::getenv("RT_DRAIN_LEAF_DIV")) ta.drain_leaf_div = std::max(0, std::min(64, std::atoi(e)));
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
   for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
@@ -2955,39 +3031,27 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     if (tex) hipLaunchKernelGGL(shade_reduce_kernel<true>, dim3(rblocks), dim3(kBlock), 0, stream, la);
     else hipLaunchKernelGGL(shade_reduce_kernel<false>, dim3(rblocks), dim3(kBlock), 0, stream, la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    if (stats) HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
+    HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     if (measure_tiles)
       HIP_TRY(hipMemcpyAsync(s->h_tile_cost, s->d_tile_cost, (size_t)n_tiles * 8, hipMemcpyDeviceToHost, stream),
               RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_t1, stream), RT_EDEVICE);
-    HIP_TRY(hipEventSynchronize(s->ev_t1), RT_EDEVICE);
-    if (measure_tiles) {  // measured tile costs, by tile id (render-order index i holds tile tl_dev[i])
-      const std::vector<unsigned char> key = meas_key_of(cam, tile_w, tile_h, n_samples);
-      if (s->meas_key != key) {
-        s->meas_key = key;
-        s->meas_cost.assign((size_t)tiles_x * tiles_y, -1.0f);
-        s->meas_visits.assign((size_t)tiles_x * tiles_y, -1.0f);
-      }
-      // RT_MEASURED_ORDER=2: total node visits; default: node visits per ray (a tile's mean
-      // ray cost -- where the long rays are)
-      const bool total = std::getenv("RT_MEASURED_ORDER") && std::atoi(std::getenv("RT_MEASURED_ORDER")) == 2;
-      for (int i = 0; i < n_tiles; ++i) {
-        const float v = (float)s->h_tile_cost[2 * i], r = (float)s->h_tile_cost[2 * i + 1];
-        s->meas_cost[(size_t)tl_dev[i]] = total ? v : (r > 0.0f ? v / r : 0.0f);
-        s->meas_visits[(size_t)tl_dev[i]] = v;
-      }
-    }
-    float ms = 0.f, t_a = 0.f, t_b = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[0][0], s->ev_b[0][0]), RT_EDEVICE);
-    if (stats && hipEventElapsedTime(&t_a, s->ev_t0, s->ev_a[0][0]) == hipSuccess &&
-        hipEventElapsedTime(&t_b, s->ev_t0, s->ev_b[0][0]) == hipSuccess)
-      busy.emplace_back(t_a, t_b);
-    trace_ms = ms;
-    iters = P.iters = 1;
-    reduced = true;
+    rt_scene_s::Pending& q = s->pending;
+    q.active = true;
+    q.count_work = p->count_work != 0;
+    q.measure_tiles = measure_tiles;
+    q.n_tiles = n_tiles;
+    q.tiles_x = tiles_x;
+    q.tiles_y = tiles_y;
+    q.tl_dev = tl_dev;
+    q.meas_key = meas_key_of(cam, tile_w, tile_h, n_samples);
 #ifdef RT_EXIT_TIMING
-    if (const int rc = print_exit_log(P.ta, ms, 0)) return rc;
+    q.ta = P.ta;
 #endif
+    // sync == 0: deferred -- rt_render_wait (or the scene's next call) finishes it, so the
+    // caller can enqueue another frame (on another scene handle and stream) meanwhile
+    if (p->sync == 0) return RT_OK;
+    return finish_one_pass(s, stats);
   }
   for (int live = one_pass ? 0 : n_pipes; live > 0;) {
     for (int h = 0; h < n_pipes; ++h) {

@@ -149,6 +149,7 @@ int rth_render(rth_scene_t h, int32_t device, const rt_render_params* p, float* 
   if (rc) return fail(rc, rt_last_error());
   rt_stats st{};
   rc = rt_render_tiles(ds, &cam, p, tiles.data(), (int32_t)tiles.size(), T, T, (float*)d_out, nullptr, &st);
+  if (!rc && p->sync == 0) rc = rt_render_wait(ds, &st);  // a deferred call: finished here
   if (rc) {
     std::string e = rt_last_error();
     rt_free(d_out);

@@ -108,3 +108,55 @@ def test_ineligible_scenes_take_the_step_pipeline(tmp_path, gpu):
     path = scenes.write(scenes.features(res=(24, 16)), str(tmp_path / "f.json"))
     _, st = _render(path, 1, {})
     assert st.path == rt.PATH_STEPS
+
+
+def test_deferred_frames_in_flight(tmp_path, gpu):
+    """RenderParams(sync=False): a one-pass call returns once enqueued and DeviceScene.wait()
+    finishes it.  Two scene handles on two streams keep two frames in flight (bench.py
+    --frames-in-flight 2); every frame must equal its synchronous render bit for bit, with
+    the same ray count, and a second call on a handle whose call is still deferred must
+    finish that one first (they share the workspace)."""
+    import torch
+    path = scenes.write(scenes.soup(4000, seed=9, res=(128, 96)), str(tmp_path / "s.json"))
+    sc = rt.Scene(path)
+    hs = [rt.DeviceScene(sc, 0), rt.DeviceScene(sc, 0)]
+    try:
+        T = 32
+        ids = np.arange((128 // T) * (96 // T), dtype=np.int32)
+        n = ids.size * T * T * 3
+
+        def params(seed, sync):
+            return rt.RenderParams(spp_sqrt=3, light_samples=1, use_bvh=True, seed=seed, sync=sync)
+
+        ref, ref_rays = [], []
+        buf = torch.zeros(n, dtype=torch.float32, device="cuda:0")
+        for k in range(4):
+            st = hs[0].render_tiles(ids, T, T, buf.data_ptr(), params(100 + k, True))
+            ref.append(buf.cpu().numpy().copy())
+            ref_rays.append(st.rays)
+        assert hs[0].wait().rays == 0  # nothing deferred
+        streams = [torch.cuda.Stream(device=0), torch.cuda.Stream(device=0)]
+        outs = [torch.zeros(n, dtype=torch.float32, device="cuda:0") for _ in range(2)]
+        got = {}
+        for k in range(4):
+            i = k % 2
+            st = hs[i].render_tiles(ids, T, T, outs[i].data_ptr(), params(100 + k, False), stream=streams[i].cuda_stream)
+            assert st.rays == 0 and st.path == rt.PATH_ONE_PASS  # enqueued only
+            if k >= 1:
+                j = (k - 1) % 2
+                got[k - 1] = (hs[j].wait(), outs[j].cpu().numpy().copy())
+        got[3] = (hs[1].wait(), outs[1].cpu().numpy().copy())
+        for k in range(4):
+            st, img = got[k]
+            assert st.rays == ref_rays[k] and st.path == rt.PATH_ONE_PASS
+            assert int((img.view(np.uint32) != ref[k].view(np.uint32)).sum()) == 0, k
+        # a handle's next call finishes its deferred one first
+        hs[0].render_tiles(ids, T, T, outs[0].data_ptr(), params(100, False), stream=streams[0].cuda_stream)
+        st = hs[0].render_tiles(ids, T, T, outs[1].data_ptr(), params(101, True))
+        assert st.rays == ref_rays[1]
+        assert int((outs[0].cpu().numpy().view(np.uint32) != ref[0].view(np.uint32)).sum()) == 0
+        assert int((outs[1].cpu().numpy().view(np.uint32) != ref[1].view(np.uint32)).sum()) == 0
+    finally:
+        for h in hs:
+            h.close()
+        sc.close()

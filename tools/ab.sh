@@ -7,7 +7,8 @@
 #   <workload> <build> <Mrays/s> <ms/step> <avg trace launch ms> <launches/step>
 # Workloads: head (bench.py default, 10 steps), em2/em4/em8 (rank N-1's share of an N-way
 # split), c2 (primary only, 1 spp), c3 (Antialiasing), c4 (glossy + soft shadows), c5 (4096^2
-# x 64 spp).  Extra ENV=VAL arguments are exported for every run.
+# x 64 spp).  Extra ENV=VAL arguments are exported for every run; BENCH_EXTRA="--flag ..." adds
+# bench.py arguments to every run.
 set -eo pipefail
 LIBS=${1:?builds}
 REPS=${2:-2}
@@ -34,7 +35,7 @@ for rep in $(seq 1 "$REPS"); do
   for wl in $WLS; do
     a=$(args_for "$wl")
     for lib in $LIBS; do
-      RT_LIB_DIR=ray_tracying_amd/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline $a \
+      RT_LIB_DIR=ray_tracying_amd/$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline $a ${BENCH_EXTRA:-} \
         > gpurun_out/ab_${wl}_${lib}.json 2> gpurun_out/ab_${wl}_${lib}.err
       python3 -c "import json,sys;d=json.load(open('gpurun_out/ab_${wl}_${lib}.json'));r=d['roofline'];print('$wl', '$lib', d['value'], d['ms_per_step'], r['avg_launch_ms'], r['launches_per_step'], flush=True)"
     done
