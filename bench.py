@@ -200,9 +200,11 @@ def parse():
     ap.add_argument("--ubench", default=None,
                     help="JSON of the counter-measured VALU microbenchmark (tools/pmc_ubench.py): the measured VALU "
                          "peak; default: the committed profile")
-    ap.add_argument("--frames-in-flight", type=int, default=1,
+    ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames rendered concurrently (scene handles on their own streams; one-pass scenes): the next "
-                         "frame's camera rays and the previous frame's shading fill the tail of the other's trace launch")
+                         "frame's camera rays and trace fill the tail of the other frame's trace launch; 0 (auto): 2 "
+                         "when this rank renders at most 32M samples per frame (a rank's share of a 4- or 8-way split), "
+                         "else 1 (whole frames lose: their two traversals interleave instead of overlapping at the tail)")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")
     return ap.parse_args()
@@ -416,7 +418,8 @@ def main():
     # framebuffer gathered -- only once frame k + F - 1 is enqueued, so the next frame's camera
     # rays and this frame's shading run in the idle tail of the other frame's trace launch.
     # Every frame is rendered in full and gathered; steps are timed exactly as with F = 1.
-    F = max(1, args.frames_in_flight)
+    units = len(mine) * T * T * max(1, args.spp_sqrt) ** 2
+    F = args.frames_in_flight if args.frames_in_flight > 0 else (2 if units <= 32 * 2 ** 20 else 1)
     fl_ds = [ds] + [rt.DeviceScene(scene, dev) for _ in range(F - 1)]
     fl_out = [out] + [torch.zeros_like(out) for _ in range(F - 1)]
     fl_st = [torch.cuda.Stream(device=dev) for _ in range(F)] if F > 1 else []

@@ -2925,7 +2925,16 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // ray's latency and so the launch's tail (C2, 1M units: 6 / 5 / 4 blocks 1679 / 1772 / 1790
   // Mrays/s; one rank's eighth, 13M units: 5 and 6 within 1 %)
   const int call_bpc = fuse_launch ? s->trace_blocks_per_cu_fuse : soft_launch ? s->trace_blocks_per_cu_soft : s->trace_blocks_per_cu;
-  const unsigned grid_cap = (unsigned)std::max(1, s->n_cu * (n_units <= (4LL << 20) ? std::max(1, call_bpc - 1) : call_bpc));
+  // A deferred one-pass call (another frame in flight) leaves one block per CU to the other
+  // frame's camera and shading kernels, which cannot share a CU's registers with six traversal
+  // waves per SIMD (r04, one box, two frames in flight, Mrays/s: one rank's eighth / quarter
+  // 5220-5260 / 5182-5258 with all blocks, 5291-5316 / 5630 with one fewer; one frame in flight
+  // 4918-4924 / 5404-5440).  RT_DEFER_BPC overrides.
+  int defer_free = one_pass && p->sync == 0 ? 1 : 0;
+  if (one_pass && p->sync == 0)
+    if (const char* e = std::getenv("RT_DEFER_BPC")) defer_free = std::max(0, std::atoi(e));
+  const unsigned grid_cap = (unsigned)std::max(
+      1, s->n_cu * std::max(1, (n_units <= (4LL << 20) ? std::max(1, call_bpc - 1) : call_bpc) - defer_free));
   size_t spill_need = 0;
   for (int h = 0; h < n_pipes; ++h) {
     Pipe& P = pipes[h];
@@ -3050,7 +3059,10 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
 #endif
     // sync == 0: deferred -- rt_render_wait (or the scene's next call) finishes it, so the
     // caller can enqueue another frame (on another scene handle and stream) meanwhile
-    if (p->sync == 0) return RT_OK;
+    if (p->sync == 0) {
+      if (stats) stats->path = RT_PATH_ONE_PASS;  // enqueued: rt_render_wait fills the rest
+      return RT_OK;
+    }
     return finish_one_pass(s, stats);
   }
   for (int live = one_pass ? 0 : n_pipes; live > 0;) {
