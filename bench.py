@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 #     4 SIMDs per CU = 2 instructions per CU-cycle (78.6 T lane-ops/s)
 N_CU, MAX_CLOCK_GHZ = 256, 2.4
 SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE = 2.0
-UBENCH_PROFILE = "r03_v9"  # committed counter-measured VALU microbenchmark (profiles/)
+UBENCH_PROFILE = "r04_v1"  # committed counter-measured VALU microbenchmark (profiles/)
 
 
 def valu_peak(path):
@@ -67,7 +67,7 @@ def valu_peak(path):
             return float(d["max_valu_wave_instr_per_cu_cycle"]), f"{os.path.relpath(path, ROOT)} ({d.get('label', '')})"
     return 1.0, "assumed 1 wave64 instruction per CU-cycle (no counter-measured microbenchmark found)"
 NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
-PMC_PROFILE = "r03_v8"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r04_v1"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
@@ -542,10 +542,14 @@ def main():
         "kernel": "trace_refill_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
         "launches_per_step": int(launches_all / args.steps / world),
         "trace_busy_ms_per_step": round(busy_ms_step, 3),
-        "trace_share_of_step": round(busy_ms_step / (elapsed / args.steps * 1e3), 3),
-        "launch_timing": "HIP events on each slot pipeline's stream; two pipelines overlap their launches, so "
-                         "avg_launch_ms includes time shared with the other pipeline's launch (rocprofv3 agrees: "
-                         "profiles/<label>_kernel_stats.csv); trace_busy_ms_per_step is the union of the launches",
+        # with F > 1 frames in flight the frames' launches overlap: their busy times sum past the
+        # step time, and no share of it is measured
+        "trace_share_of_step": round(busy_ms_step / (elapsed / args.steps * 1e3), 3) if F == 1 else None,
+        "launch_timing": "HIP events around each trace launch on its call's stream (rocprofv3 agrees: "
+                         "profiles/<label>_kernel_stats.csv); trace_busy_ms_per_step is the union of one frame's "
+                         "launches (the step pipeline's slot pipelines overlap theirs).  With config.frames_in_flight "
+                         "> 1 the frames' launches overlap each other, so avg_launch_ms includes time shared with "
+                         "the other frame's and trace_share_of_step is null",
     }
     if args.scene:  # C1-C4: a few primitives, LDS/L1-resident -- no roofline claim
         roofline = {"bound": None, "frac": None, "achieved": None, "peak": None, "unit": None, "traffic": None,

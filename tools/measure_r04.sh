@@ -5,7 +5,7 @@
 # (FETCH_SIZE, WRITE_SIZE, the VALU set; one pass each, dispatches serialised by the profiler)
 # of the headline frame and of C5 (4096^2 x 64 spp), and the counter-measured VALU microbenchmark; the full headline bench (with the CPU
 # baseline) carrying the PMC summaries just measured; the other BASELINE configs (C2, C3,
-# C4, C5).  The per-rank shares of split frames: tools/measure_r03_shares.sh.  Everything lands
+# C4, C5).  The per-rank shares of split frames: tools/measure_r04_shares.sh.  Everything lands
 # in gpurun_out/.
 set -eo pipefail
 L=${1:?label}
@@ -40,6 +40,8 @@ python3 tools/pmc_ubench.py --dir gpurun_out/${L}_ubench_pmc --out gpurun_out/${
 echo "bench $(date +%T)"
 timeout -k 10 600 python3 bench.py --steps 10 --warmup 2 --pmc-traffic gpurun_out/${L}_pmc_traffic.json --pmc-valu gpurun_out/${L}_pmc_valu.json --ubench gpurun_out/${L}_ubench_valu_pmc.json > gpurun_out/${L}_bench.json 2> gpurun_out/${L}_bench.err
 cat gpurun_out/${L}_bench.json
+echo "issue-mix microbenchmark $(date +%T)"
+timeout -k 10 200 tools/bin/ubench_mix > gpurun_out/${L}_ubench_mix.txt 2>&1
 echo "configs $(date +%T)"
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --primary-only --spp-sqrt 1 > gpurun_out/${L}_c2_primary_only_bench.json 2> gpurun_out/${L}_c2.err
 timeout -k 10 300 python3 bench.py --steps 3 --scene $B/Antialiasing.json > gpurun_out/${L}_c3_antialiasing_bench.json 2> gpurun_out/${L}_c3.err
