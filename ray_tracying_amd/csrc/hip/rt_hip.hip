@@ -389,6 +389,14 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
   }
 }
 
+// a wave-uniform value in an SGPR of its own (opaque to the optimiser: not re-fused with the
+// wide load it came from)
+__device__ __forceinline__ int sgpr_copy(int v) {
+  int r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
+  return r;
+}
+
 // cswap on non-negative (or +inf) floats compared as integers (node_visit's child order)
 __device__ __forceinline__ void cswap_bits(float& ta, int& ca, float& tb, int& cb) {
   const int ia = __float_as_int(ta), ib = __float_as_int(tb);
@@ -553,32 +561,49 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr int kNoItem = -1;
 __device__ __forceinline__ bool is_leaf_item(int e) { return e != kNoItem && e < 0; }
 
+// The lane's stack pointer is one word, the LDS byte offset of its next free entry:
+// w = sp * kStackRow + threadIdx.x * 8 (entries are lane-minor rows of the block's 8-B
+// (entry, t_near) pairs), so a push or pop is one add and the lane's own base never has to
+// stay live across the traversal loop (r04: kept apart, the base was spilled to scratch and
+// reloaded on every node visit and pop).  sp = w / kStackRow; w % kStackRow is the lane's
+// column; entries from lds_entries on live in the HBM spill area at gtid.
+constexpr int kStackRow = kBlock * 8;
+static_assert((kStackRow & (kStackRow - 1)) == 0, "stack rows are a power of two");
+__device__ __forceinline__ int stack_depth(int w) { return w / kStackRow; }
+__device__ __forceinline__ int stack_empty_word(int w) { return w & (kStackRow - 1); }
+
 struct LaneStack {
-  int2* e;     // LDS (entry, t_near bits), lane-minor: e[i * kBlock]
+  char* lds;   // the block's LDS stack area
   int2* spill; // entries past lds_entries: spill[(i - lds) * n_threads + gtid]
 };
 
-__device__ __forceinline__ void stack_push(const TraceArgs& a, const LaneStack& S, int& sp, int gtid, int e, float t) {
-  if (sp < a.lds_entries) S.e[sp * kBlock] = make_int2(e, __float_as_int(t));
+__device__ __forceinline__ int2* stack_at(const TraceArgs& a, const LaneStack& S, int w_col, int i, int gtid) {
+  return i < a.lds_entries ? reinterpret_cast<int2*>(S.lds + w_col + i * kStackRow)
+                           : S.spill + (size_t)(i - a.lds_entries) * a.n_threads + gtid;
+}
+
+__device__ __forceinline__ void stack_push(const TraceArgs& a, const LaneStack& S, int& w, int gtid, int e, float t) {
+  const int sp = stack_depth(w);
+  if (sp < a.lds_entries) *reinterpret_cast<int2*>(S.lds + w) = make_int2(e, __float_as_int(t));
   else S.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = make_int2(e, __float_as_int(t));
-  ++sp;
+  w += kStackRow;
 }
 
 // Pops entries until one is still within the bound (each popped entry is re-culled against
 // the bound current now); kNoItem when the stack empties.  Wave-uniform fast path when no
 // lane's stack reaches into the HBM spill area.
-__device__ __forceinline__ int stack_pop_live(const TraceArgs& a, const LaneStack& S, int& sp, int gtid, float lim) {
-  if (__ballot(sp > a.lds_entries) == 0ull) {
-    while (sp > 0) {
-      --sp;
-      const int2 v = S.e[sp * kBlock];
+__device__ __forceinline__ int stack_pop_live(const TraceArgs& a, const LaneStack& S, int& w, int gtid, float lim) {
+  if (__ballot(w >= (a.lds_entries + 1) * kStackRow) == 0ull) {
+    while (w >= kStackRow) {
+      w -= kStackRow;
+      const int2 v = *reinterpret_cast<const int2*>(S.lds + w);
       if (!(__int_as_float(v.y) > lim)) return v.x;
     }
     return kNoItem;
   }
-  while (sp > 0) {
-    --sp;
-    const int2 v = sp < a.lds_entries ? S.e[sp * kBlock] : S.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid];
+  while (w >= kStackRow) {
+    w -= kStackRow;
+    const int2 v = *stack_at(a, S, stack_empty_word(w), stack_depth(w), gtid);
     if (!(__int_as_float(v.y) > lim)) return v.x;
   }
   return kNoItem;
@@ -587,13 +612,11 @@ __device__ __forceinline__ int stack_pop_live(const TraceArgs& a, const LaneStac
 // Drain: removes and returns the lane's bottom stack entry -- pushed first, so the farthest
 // pending subtree of the query -- and moves the others down one, so sp never exceeds the
 // serial traversal's depth bound (the order of the rest is kept).
-__device__ __forceinline__ int2 stack_take_bottom(const TraceArgs& a, const LaneStack& S, int& sp, int gtid) {
-  auto at = [&](int i) -> int2* {
-    return i < a.lds_entries ? S.e + i * kBlock : S.spill + (size_t)(i - a.lds_entries) * a.n_threads + gtid;
-  };
-  const int2 b = *at(0);
-  for (int i = 1; i < sp; ++i) *at(i - 1) = *at(i);
-  --sp;
+__device__ __forceinline__ int2 stack_take_bottom(const TraceArgs& a, const LaneStack& S, int& w, int gtid) {
+  const int col = stack_empty_word(w), sp = stack_depth(w);
+  const int2 b = *stack_at(a, S, col, 0, gtid);
+  for (int i = 1; i < sp; ++i) *stack_at(a, S, col, i - 1, gtid) = *stack_at(a, S, col, i, gtid);
+  w -= kStackRow;
   return b;
 }
 
@@ -614,7 +637,7 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
 template <bool kCount>
 __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, float lim, int node,
-                                          const LaneStack& S, int& sp, int gtid, unsigned int& nbox,
+                                          const LaneStack& S, int& w, int gtid, unsigned int& nbox,
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
@@ -696,19 +719,19 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   // at sp, sp+v3, sp+v3+v2 -- offsets counting only the children entered -- leave exactly
   // those below the new top whatever the order (a missed one lands on the next slot and is
   // overwritten or abandoned).
-  if (__ballot(sp + 3 > a.lds_entries) == 0ull) {
-    int2* st = S.e + sp * kBlock;
-    st[0] = make_int2(c[3], __float_as_int(t[3]));
-    st[(int)v3 * kBlock] = make_int2(c[2], __float_as_int(t[2]));
-    st[((int)v3 + (int)v2) * kBlock] = make_int2(c[1], __float_as_int(t[1]));
-    sp += (int)v3 + (int)v2 + (int)v1;
+  if (__ballot(w >= (a.lds_entries - 2) * kStackRow) == 0ull) {  // sp + 3 <= lds_entries in every lane
+    char* st = S.lds + w;
+    *reinterpret_cast<int2*>(st) = make_int2(c[3], __float_as_int(t[3]));
+    *reinterpret_cast<int2*>(st + (int)v3 * kStackRow) = make_int2(c[2], __float_as_int(t[2]));
+    *reinterpret_cast<int2*>(st + ((int)v3 + (int)v2) * kStackRow) = make_int2(c[1], __float_as_int(t[1]));
+    w += ((int)v3 + (int)v2 + (int)v1) * kStackRow;
   } else {
-    if (v3) stack_push(a, S, sp, gtid, c[3], t[3]);
-    if (v2) stack_push(a, S, sp, gtid, c[2], t[2]);
-    if (v1) stack_push(a, S, sp, gtid, c[1], t[1]);
+    if (v3) stack_push(a, S, w, gtid, c[3], t[3]);
+    if (v2) stack_push(a, S, w, gtid, c[2], t[2]);
+    if (v1) stack_push(a, S, w, gtid, c[1], t[1]);
   }
   if (__float_as_int(t[0]) != 0x7f800000) return c[0];
-  return stack_pop_live(a, S, sp, gtid, lim);
+  return stack_pop_live(a, S, w, gtid, lim);
 }
 
 // Refill kernel.  Lanes that finished their query are handed new slots (from the wave's
@@ -763,7 +786,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   unsigned long long dg_any_rays = 0, dg_any_box = 0;
   unsigned int nvc = 0, nrc = 0;  // count_work: nvisit / nrays at the wave's last work fetch (measured tile costs)
   int cost_tile = -1;    // render-order tile of the wave's last fetched group
+#ifdef RT_SGPR_SPLIT
+  // the loop's scalar parameters as separate SGPRs: loaded as part of a wide kernel-argument
+  // load, a field spilled to a VGPR lane is restored with its whole 8-dword tuple (8
+  // v_readlane per use at the loop head, r04)
+  TraceArgs la = ta;
+  la.refill_min = sgpr_copy(ta.refill_min);
+  la.leaf_min = sgpr_copy(ta.leaf_min);
+  la.lds_entries = sgpr_copy(ta.lds_entries);
+  const TraceArgs& a = la;
+#else
   const TraceArgs& a = ta;
+#endif
   const unsigned int any = *ta.any_query;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ta.host_flag = any;  // read by the host after the step
   if (any == 0u) return;
@@ -782,14 +816,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   float lim = 0.0f;     // cull bound of the query (cull_limit), refreshed after each leaf test
   Query q;
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
-  int sp = 0;
-  const LaneStack S{reinterpret_cast<int2*>(lds_stack) + threadIdx.x, reinterpret_cast<int2*>(a.spill)};
+  int sw = (int)threadIdx.x * 8;  // the lane's stack word (LaneStack): empty
+  const LaneStack S{reinterpret_cast<char*>(lds_stack), reinterpret_cast<int2*>(a.spill)};
   // a query was set up in q: start its traversal at the root (BVH::intersect_linear tests
   // every primitive at once, acceleration.cpp:124-139, and leaves nothing to traverse)
   auto start_traversal = [&]() {
     h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
     lim = cull_limit(a, q, h);
-    sp = 0;
+    sw = stack_empty_word(sw);
     item = (a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem;
     if (a.c.n_prims > 0 && !a.c.use_bvh)
       test_prims<kCount, kPlanesOnly>(a, slot, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
@@ -991,18 +1025,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         test_prims<kCount, kPlanesOnly>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
                                         true, h, nprim);
         lim = cull_limit(a, q, h);
-        item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
+        item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
       }
       RT_PT_MARK(1);  // leaf phase
     }
     // node phase
 #ifdef RT_PHASE_TIMING
     if (__ballot(item >= 0) != 0ull) {
-      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
       RT_PT_MARK(2);  // node phase
     }
 #else
-    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
 #endif
   }
   // ---- drain (drain_help: the queue is dry).  A query still traversing keeps its lane (its
@@ -1053,13 +1087,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       }
       if (own >= 0 && item == kNoItem) {
         own = -1;
-        sp = 0;
+        sw = stack_empty_word(sw);
       }
       // an owner whose traversal and helpers are done settles (and may start its next query)
       if (slot >= 0 && item == kNoItem && nh == 0) settle();
       if (__ballot(slot >= 0) == 0ull) break;
       // pair free lanes with lanes that have stack entries (k-th free lane, k-th donor)
-      const bool can_give = item != kNoItem && sp > 0;
+      const bool can_give = item != kNoItem && sw >= kStackRow;
       const uint64_t D = __ballot(can_give), I = __ballot(slot < 0 && own < 0);
       if (D != 0ull && I != 0ull) {
         const int k = min(__popcll(D), __popcll(I));
@@ -1074,7 +1108,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           if (lane == __builtin_amdgcn_readlane(rootv, dl)) ++nh;
         }
         int2 ent = make_int2(kNoItem, 0);
-        if (can_give && __popcll(D & lane_lt) < k) ent = stack_take_bottom(a, S, sp, gtid);
+        if (can_give && __popcll(D & lane_lt) < k) ent = stack_take_bottom(a, S, sw, gtid);
         const int s2 = src >= 0 ? src : lane;
         const int ge = __shfl(ent.x, s2), gt = __shfl(ent.y, s2), rs = __shfl(rootv, s2);
         const int qs = src >= 0 ? rs : lane;  // receivers copy their owner's query
@@ -1099,7 +1133,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           own = rs;
           h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
           lim = rl;
-          sp = 0;
+          sw = stack_empty_word(sw);
           item = __int_as_float(gt) > rl ? kNoItem : ge;
         }
       }
@@ -1125,10 +1159,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           test_prims<kCount, kPlanesOnly, true>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax,
                                                 q.par, true, h, nprim);
           lim = cull_limit(a, q, h);
-          item = h.done ? kNoItem : stack_pop_live(a, S, sp, gtid, lim);
+          item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
         }
       }
-      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sp, gtid, nbox, dg_any_box, nvisit);
+      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
     }
   }
   RT_PT_FLUSH
