@@ -340,6 +340,13 @@ __device__ __forceinline__ bool plane_leaf_fast_ok(const PrimA& P, const Ray& r,
   return ok;
 }
 
+// A scene array element at a 32-bit byte offset from its base: global loads with the base in
+// SGPRs and the offset in one VGPR, no 64-bit address arithmetic per access (node indices <
+// 2^26 and primitive indices < 2^24 are enforced by rt_scene_create).
+__device__ __forceinline__ const float4* at_byte(const float4* base, uint32_t off) {
+  return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
+}
+
 // Tests primitives [first, first + cnt) against the lane's query.  Planes-only scenes without
 // textures store a new closest hit's record (Plane::intersect's hit point and the precomputed
 // normal, shapes.cpp:472-480, and the material) to the slot's hit record when it is found --
@@ -350,7 +357,7 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
                                            float tmax, uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
   for (int k = 0; k < cnt; ++k) {
     const int pi = first + k;
-    const float4* rec = a.c.prims + (size_t)pi * a.c.prim_stride4;
+    const float4* rec = at_byte(a.c.prims, (uint32_t)pi * ((uint32_t)a.c.prim_stride4 << 4));  // pi < 2^24
     PrimA P;
     load_prim_a(rec, P);
     float t;
@@ -393,7 +400,7 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
 // wide load it came from)
 __device__ __forceinline__ int sgpr_copy(int v) {
   int r;
-  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(v));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(__builtin_amdgcn_readfirstlane(v)));
   return r;
 }
 
@@ -650,7 +657,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2 * nn);
   const int4 qc = *reinterpret_cast<const int4*>(nd + 3 * nn);
 #else
-  const float4* nd = a.c.nodes + (size_t)node * 4;
+  const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
   const float4 g = nd[0];
   const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
   const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
@@ -786,18 +793,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   unsigned long long dg_any_rays = 0, dg_any_box = 0;
   unsigned int nvc = 0, nrc = 0;  // count_work: nvisit / nrays at the wave's last work fetch (measured tile costs)
   int cost_tile = -1;    // render-order tile of the wave's last fetched group
-#ifdef RT_SGPR_SPLIT
   // the loop's scalar parameters as separate SGPRs: loaded as part of a wide kernel-argument
   // load, a field spilled to a VGPR lane is restored with its whole 8-dword tuple (8
-  // v_readlane per use at the loop head, r04)
+  // v_readlane per use at the loop head; r04 A/B: headline +5 %, one rank's eighth +4 %, C5 +6 %)
   TraceArgs la = ta;
   la.refill_min = sgpr_copy(ta.refill_min);
   la.leaf_min = sgpr_copy(ta.leaf_min);
   la.lds_entries = sgpr_copy(ta.lds_entries);
   const TraceArgs& a = la;
-#else
-  const TraceArgs& a = ta;
-#endif
   const unsigned int any = *ta.any_query;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ta.host_flag = any;  // read by the host after the step
   if (any == 0u) return;
@@ -818,13 +821,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
   int sw = (int)threadIdx.x * 8;  // the lane's stack word (LaneStack): empty
   const LaneStack S{reinterpret_cast<char*>(lds_stack), reinterpret_cast<int2*>(a.spill)};
+  // the first item of every traversal (wave-uniform, in an SGPR of its own: as a VGPR constant
+  // it was spilled and reloaded in the leaf loop)
+  const int root_item = sgpr_copy((a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem);
   // a query was set up in q: start its traversal at the root (BVH::intersect_linear tests
   // every primitive at once, acceleration.cpp:124-139, and leaves nothing to traverse)
   auto start_traversal = [&]() {
     h = HitState{__builtin_inff(), 0x7fffffff, -1, false};
     lim = cull_limit(a, q, h);
     sw = stack_empty_word(sw);
-    item = (a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem;
+    item = root_item;
     if (a.c.n_prims > 0 && !a.c.use_bvh)
       test_prims<kCount, kPlanesOnly>(a, slot, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
   };
@@ -2374,6 +2380,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
       (d->n_prims > d->n_unbounded && (d->n_nodes <= 0 || !d->nodes)) || d->n_unbounded < 0 ||
       d->n_unbounded > d->n_prims || (d->n_prims > 0 && (d->n_ref_leaves <= 0 || !d->ref_leaf_boxes)))
     return fail(RT_EINVAL, "rt_scene_create: inconsistent primitive/node arrays (at most 2^24 - 1 primitives)");
+  if (d->n_nodes < 0 || d->n_nodes >= (1 << 26))
+    return fail(RT_EINVAL, "rt_scene_create: at most 2^26 - 1 BVH4 nodes");
   if (d->stack_bound < 1 || d->stack_bound > 4096) return fail(RT_EINVAL, "rt_scene_create: stack_bound out of range");
   if (d->prim_stride != 64 && d->prim_stride != 128)
     return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
