@@ -2202,7 +2202,7 @@ struct rt_scene_s {
     int n_tiles = 0, tiles_x = 0, tiles_y = 0;
     std::vector<int32_t> tl_dev;
     std::vector<unsigned char> meas_key;
-#ifdef RT_EXIT_TIMING
+#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING)
     TraceArgs ta{};
 #endif
   } pending;
@@ -2576,6 +2576,15 @@ static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
   HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[0][0], s->ev_b[0][0]), RT_EDEVICE);
 #ifdef RT_EXIT_TIMING
   if (const int rc = print_exit_log(q.ta, ms, 0)) return rc;
+#endif
+#ifdef RT_PHASE_TIMING
+  {
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIP_TRY(hipMemcpy(pt, q.ta.counters + 64, sizeof(pt), hipMemcpyDeviceToHost), RT_EDEVICE);
+    const double tot = (double)(pt[0] + pt[1] + pt[2] + pt[3]);
+    std::fprintf(stderr, "[rt phase] refill %.3f (%llu), leaf %.3f (%llu), node %.3f (%llu), control %.3f (%llu) of %.3g wave-ticks\n",
+                 pt[0] / tot, pt[4], pt[1] / tot, pt[5], pt[2] / tot, pt[6], pt[3] / tot, pt[7], tot);
+  }
 #endif
   s->last_iters = 1;
   if (!stats) return RT_OK;
@@ -3096,7 +3105,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
     q.tiles_y = tiles_y;
     q.tl_dev = tl_dev;
     q.meas_key = meas_key_of(cam, tile_w, tile_h, n_samples);
-#ifdef RT_EXIT_TIMING
+#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING)
     q.ta = P.ta;
 #endif
     // sync == 0: deferred -- rt_render_wait (or the scene's next call) finishes it, so the

@@ -40,7 +40,8 @@ def test_fma_only_in_powf_div_and_culling(ir):
     # Markstein quotient (rt_div.h: exact remainder and correction, == IEEE division,
     # tests/test_div.py), and the packed (v2f32) fma of the BVH slab test, which only culls
     # (padded boxes, exact re-check of every candidate hit).  Every scalar f32 fma is one of
-    # rt_div_by's two: each fma.f32 call site pairs with an fneg (the remainder's -q0).
+    # rt_div_by's two, whose first takes an fneg (the remainder's -q0); CSE may merge one of a
+    # pair across identical quotients, so the count need not be even.
     f32_fma = ir.count("call float @llvm.fma.f32")
-    assert f32_fma % 2 == 0 and f32_fma <= 2 * ir.count("fneg float")
+    assert f32_fma <= 2 * ir.count("fneg float")
     assert "@llvm.fma.v2f32" in ir  # the culling slab is where the packed form is expected
