@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 #     4 SIMDs per CU = 2 instructions per CU-cycle (78.6 T lane-ops/s)
 N_CU, MAX_CLOCK_GHZ = 256, 2.4
 SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE = 2.0
-UBENCH_PROFILE = "r04_v1"  # committed counter-measured VALU microbenchmark (profiles/)
+UBENCH_PROFILE = "r04_v3"  # committed counter-measured VALU microbenchmark (profiles/)
 
 
 def valu_peak(path):
@@ -67,7 +67,7 @@ def valu_peak(path):
             return float(d["max_valu_wave_instr_per_cu_cycle"]), f"{os.path.relpath(path, ROOT)} ({d.get('label', '')})"
     return 1.0, "assumed 1 wave64 instruction per CU-cycle (no counter-measured microbenchmark found)"
 NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
-PMC_PROFILE = "r04_v1"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r04_v3"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
