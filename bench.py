@@ -202,9 +202,10 @@ def parse():
                          "peak; default: the committed profile")
     ap.add_argument("--frames-in-flight", type=int, default=0,
                     help="frames rendered concurrently (scene handles on their own streams; one-pass scenes): the next "
-                         "frame's camera rays and trace fill the tail of the other frame's trace launch; 0 (auto): 2 "
-                         "when this rank renders at most 32M samples per frame (a rank's share of a 4- or 8-way split), "
-                         "else 1 (whole frames lose: their two traversals interleave instead of overlapping at the tail)")
+                         "frame's camera rays and trace fill the tail of the other frame's trace launch; 0 (auto): 3 "
+                         "when this rank renders at most 4M samples per frame (C2), 2 up to 32M (a rank's share of a 4- "
+                         "or 8-way split), else 1 (whole frames lose: their traversals interleave instead of overlapping "
+                         "at the tail)")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")
     return ap.parse_args()
@@ -419,7 +420,10 @@ def main():
     # rays and this frame's shading run in the idle tail of the other frame's trace launch.
     # Every frame is rendered in full and gathered; steps are timed exactly as with F = 1.
     units = len(mine) * T * T * max(1, args.spp_sqrt) ** 2
-    F = args.frames_in_flight if args.frames_in_flight > 0 else (2 if units <= 32 * 2 ** 20 else 1)
+    # auto (one box, r04): C2's 1.05M samples 2,606 / 2,786 / 2,690 Mrays/s at F = 2 / 3 / 4; one
+    # rank's eighth (18M) 6,322 at F = 2, 5,926 at F = 3; whole frames keep one
+    F = args.frames_in_flight if args.frames_in_flight > 0 else (
+        3 if units <= 4 * 2 ** 20 else 2 if units <= 32 * 2 ** 20 else 1)
     fl_ds = [ds] + [rt.DeviceScene(scene, dev) for _ in range(F - 1)]
     fl_out = [out] + [torch.zeros_like(out) for _ in range(F - 1)]
     fl_st = [torch.cuda.Stream(device=dev) for _ in range(F)] if F > 1 else []

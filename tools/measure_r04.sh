@@ -43,7 +43,7 @@ cat gpurun_out/${L}_bench.json
 echo "issue-mix microbenchmark $(date +%T)"
 timeout -k 10 200 tools/bin/ubench_mix > gpurun_out/${L}_ubench_mix.txt 2>&1
 echo "configs $(date +%T)"
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 10 --primary-only --spp-sqrt 1 > gpurun_out/${L}_c2_primary_only_bench.json 2> gpurun_out/${L}_c2.err
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 30 --primary-only --spp-sqrt 1 > gpurun_out/${L}_c2_primary_only_bench.json 2> gpurun_out/${L}_c2.err
 timeout -k 10 300 python3 bench.py --steps 3 --scene $B/Antialiasing.json > gpurun_out/${L}_c3_antialiasing_bench.json 2> gpurun_out/${L}_c3.err
 timeout -k 10 300 python3 bench.py --steps 2 --scene $B/glossy_reflection.json --light-radius 1.0 --light-samples 4 > gpurun_out/${L}_c4_glossy_soft_bench.json 2> gpurun_out/${L}_c4.err
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 --res 4096 --spp-sqrt 8 --pmc-traffic gpurun_out/${L}_c5_pmc_traffic.json --pmc-valu gpurun_out/${L}_c5_pmc_valu.json --ubench gpurun_out/${L}_ubench_valu_pmc.json > gpurun_out/${L}_c5_4096_64spp_1gpu_bench.json 2> gpurun_out/${L}_c5.err
