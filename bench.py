@@ -158,6 +158,45 @@ def spawn_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def rank_summary(dist, coll: str, world: int, steps: int, wall_s: float, render_ms: float, gather_ms: float,
+                 rays: float) -> dict:
+    """Per-rank timing of the timed steps, all-gathered so rank 0's line shows which rank was slow
+    and what the collective cost.  Per rank and per step: `wall_ms` -- its own
+    time from the start barrier until its last frame was gathered (before the end barrier, which
+    makes every rank wait for the slowest); `render_ms` -- the GPU time of its frames' kernels
+    (rt_stats.kernel_ms: HIP events from a frame's first kernel to its last, after any earlier work
+    on the stream -- frames in flight overlap, so with frames_in_flight > 1 the sum can exceed the
+    step); `gather_ms` -- its part of the framebuffer gather (HIP events around
+    torch.distributed.gather on the collective's stream, or host time over gloo), including the
+    wait for the other ranks to arrive; `rays`.  slowest_rank = the largest render_ms."""
+    import torch
+    mine = torch.tensor([wall_s * 1e3 / steps, render_ms / steps, gather_ms / steps, rays / steps],
+                        dtype=torch.float64, device=coll)
+    if dist is not None and world > 1:
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+    else:
+        parts = [mine]
+    rows = [p.cpu().tolist() for p in parts]
+    render = [r[1] for r in rows]
+    slow = max(range(len(rows)), key=lambda i: render[i])
+    return {
+        "n": len(rows),
+        "wall_ms_per_step": [round(r[0], 4) for r in rows],
+        "render_ms_per_step": [round(r[1], 4) for r in rows],
+        "gather_ms_per_step": [round(r[2], 4) for r in rows],
+        "rays_per_step": [int(r[3]) for r in rows],
+        "slowest_rank": slow,
+        "slowest_render_ms_per_step": round(render[slow], 4),
+        "fastest_render_ms_per_step": round(min(render), 4),
+        "mean_render_ms_per_step": round(sum(render) / len(render), 4),
+        "definitions": "per rank and step: wall = own time from the start barrier to its last gather (before the "
+                       "end barrier); render = GPU time of its frames' kernels (rt_stats.kernel_ms; overlapping "
+                       "frames in flight each counted); gather = its torch.distributed.gather incl. waiting for the "
+                       "other ranks (HIP events on GPU, host time over gloo); slowest_rank = largest render",
+    }
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -207,7 +246,8 @@ def parse():
                          "or 8-way split), else 1 (whole frames lose: their traversals interleave instead of overlapping "
                          "at the tail)")
     ap.add_argument("--dump-frame", default=None,
-                    help="after timing, render one frame at --seed, gather it and save it (rank 0) as .npy")
+                    help="after timing, render the frame at --seed with the timed steps' calls (same frames in "
+                         "flight), gather it and save it (rank 0) as an (H, W, 3) .npy; unrendered tiles NaN")
     return ap.parse_args()
 
 
@@ -314,14 +354,18 @@ def main():
     backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
     dist = None
     if args.dry_run:  # launcher check without a GPU: process group, one collective, the rank count
+        ranks_in_group = 1
         if world > 1:
             import torch.distributed as dist
             dist.init_process_group("gloo")
             t = torch.tensor([1.0])
             dist.all_reduce(t)
-            world = int(t.item())
+            ranks_in_group = int(t.item())
+        # the per-rank summary's collective with stand-in timings (rank r: r + 1 ms of render per step)
+        summ = rank_summary(dist, "cpu", world, 1, 0.001 * (rank + 2), 1.0 * (rank + 1), 0.5, 1000.0 * (rank + 1))
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_in_group": world}), flush=True)
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_in_group": ranks_in_group, "ranks": summ}),
+                  flush=True)
         if dist:
             dist.destroy_process_group()
         return
@@ -405,14 +449,43 @@ def main():
         f"{scene.info.tree_depth}, load+build {load_s:.1f} s; {len(mine)} tiles on cuda:{dev}")
 
     params = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=args.seed)
+    timing = {"on": False, "render_ms": 0.0, "gather_s": 0.0, "gather_ev": []}
+
+    def gather(buf):
+        """Framebuffer gather to rank 0 over RCCL / xGMI; timed (HIP events on the collective's
+        stream, or host time over gloo) during the timed steps."""
+        nonlocal gathered
+        if not dist:
+            return
+        if timing["on"] and coll != "cpu":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            gathered = tl.gather_to_root(dist, buf, rank, world)
+            e1.record()
+            timing["gather_ev"].append((e0, e1))
+        else:
+            t = time.perf_counter()
+            gathered = tl.gather_to_root(dist, buf if coll != "cpu" else buf.cpu(), rank, world)
+            if timing["on"]:
+                timing["gather_s"] += time.perf_counter() - t
 
     def step(seed):
-        nonlocal gathered
         params.seed = seed
         st = ds.render_tiles(mine, T, T, out.data_ptr(), params)
-        if dist:  # framebuffer gather to rank 0 over RCCL / xGMI
-            gathered = tl.gather_to_root(dist, out if coll != "cpu" else out.cpu(), rank, world)
+        gather(out)
         return st
+
+    # ---- instrumented frame: algorithmic bytes per ray (same seed as the first timed step); its
+    # path decides whether frames in flight apply (one-pass calls only)
+    cp = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=args.seed,
+                         count_work=True)
+    cst = ds.render_tiles(mine, T, T, out.data_ptr(), cp)
+    prim_bytes = scene.info.prim_stride  # 64 B planes / 128 B transformed records
+    bytes_per_ray = (NODE_BYTES * cst.node_visits + prim_bytes * cst.prim_tests) / max(cst.rays, 1)
+    log(f"[rank {rank}] instrumented: rays {cst.rays}, node visits {cst.node_visits} "
+        f"({cst.node_visits / max(cst.rays, 1):.2f}/ray), box tests {cst.box_tests} "
+        f"({cst.box_tests / max(cst.rays, 1):.1f}/ray), prim tests {cst.prim_tests} "
+        f"({cst.prim_tests / max(cst.rays, 1):.2f}/ray), {bytes_per_ray:.0f} B/ray")
 
     # Frames in flight (--frames-in-flight F > 1): frame k renders on scene handle k % F and its
     # own HIP stream, deferred (RenderParams.sync=False), and is finished -- waited for, its
@@ -421,9 +494,11 @@ def main():
     # Every frame is rendered in full and gathered; steps are timed exactly as with F = 1.
     units = len(mine) * T * T * max(1, args.spp_sqrt) ** 2
     # auto (one box, r04): C2's 1.05M samples 2,606 / 2,786 / 2,690 Mrays/s at F = 2 / 3 / 4; one
-    # rank's eighth (18M) 6,322 at F = 2, 5,926 at F = 3; whole frames keep one
+    # rank's eighth (18M) 6,322 at F = 2, 5,926 at F = 3; whole frames keep one.  Step-pipeline
+    # calls (reflection, refraction, soft lights) complete before returning: nothing to overlap
+    # (ADVICE r04), so they keep one frame in flight
     F = args.frames_in_flight if args.frames_in_flight > 0 else (
-        3 if units <= 4 * 2 ** 20 else 2 if units <= 32 * 2 ** 20 else 1)
+        1 if cst.path != rt.PATH_ONE_PASS else 3 if units <= 4 * 2 ** 20 else 2 if units <= 32 * 2 ** 20 else 1)
     fl_ds = [ds] + [rt.DeviceScene(scene, dev) for _ in range(F - 1)]
     fl_out = [out] + [torch.zeros_like(out) for _ in range(F - 1)]
     fl_st = [torch.cuda.Stream(device=dev) for _ in range(F)] if F > 1 else []
@@ -435,15 +510,14 @@ def main():
         fl_ds[i].render_tiles(mine, T, T, fl_out[i].data_ptr(), p, stream=fl_st[i].cuda_stream)
 
     def finish(k):
-        nonlocal gathered
         i = k % F
-        st = fl_ds[i].wait()
-        if dist:  # the frame is complete (wait): gather it to rank 0 over RCCL / xGMI
-            gathered = tl.gather_to_root(dist, fl_out[i] if coll != "cpu" else fl_out[i].cpu(), rank, world)
+        st = fl_ds[i].wait()  # a deferred frame, or the held stats of one that completed in issue()
+        gather(fl_out[i])  # the frame is complete (wait)
         return st
 
     def run_frames(seeds):
-        """Render the frames (F in flight) and return their stats in order."""
+        """Render the frames (F in flight) and return their stats in order; the last frame's
+        buffer is fl_out[(len(seeds) - 1) % F] (gathered: `gathered`)."""
         if F == 1:
             return [step(sd) for sd in seeds]
         sts = []
@@ -455,17 +529,6 @@ def main():
             sts.append(finish(k))
         return sts
 
-    # ---- instrumented frame: algorithmic bytes per ray (same seed as the first timed step)
-    cp = rt.RenderParams(spp_sqrt=args.spp_sqrt, light_samples=args.light_samples, use_bvh=True, seed=args.seed,
-                         count_work=True)
-    cst = ds.render_tiles(mine, T, T, out.data_ptr(), cp)
-    prim_bytes = scene.info.prim_stride  # 64 B planes / 128 B transformed records
-    bytes_per_ray = (NODE_BYTES * cst.node_visits + prim_bytes * cst.prim_tests) / max(cst.rays, 1)
-    log(f"[rank {rank}] instrumented: rays {cst.rays}, node visits {cst.node_visits} "
-        f"({cst.node_visits / max(cst.rays, 1):.2f}/ray), box tests {cst.box_tests} "
-        f"({cst.box_tests / max(cst.rays, 1):.1f}/ray), prim tests {cst.prim_tests} "
-        f"({cst.prim_tests / max(cst.rays, 1):.2f}/ray), {bytes_per_ray:.0f} B/ray")
-
     run_frames([args.seed + 1000 + w for w in range(args.warmup)])
     torch.cuda.synchronize()
     if dist:
@@ -475,19 +538,26 @@ def main():
     rays = 0
     trace_ms = 0.0
     busy_ms = 0.0
+    render_ms = 0.0
     launches = 0
     one_pass = True
+    timing["on"] = True
     for st in run_frames([args.seed + k for k in range(args.steps)]):
         one_pass = one_pass and st.path == rt.PATH_ONE_PASS
         rays += st.rays
         trace_ms += st.trace_ms
         busy_ms += st.trace_busy_ms
+        render_ms += st.kernel_ms
         launches += st.iterations
+    timing["on"] = False
     torch.cuda.synchronize()
+    own_wall = time.perf_counter() - t0  # before the end barrier: this rank's own time
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gather_ms = timing["gather_s"] * 1e3 + sum(e0.elapsed_time(e1) for e0, e1 in timing["gather_ev"])
+    ranks = rank_summary(dist, coll, world, args.steps, own_wall, render_ms, gather_ms, float(rays))
 
     tot = torch.tensor([float(rays), trace_ms, float(launches), bytes_per_ray * rays, busy_ms], dtype=torch.float64,
                        device=coll)
@@ -501,12 +571,24 @@ def main():
     if rank == 0 and dist:  # sanity: the gathered frame has every pixel, all finite
         img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H, deal)
         assert np.isfinite(img).all()
-    if args.dump_frame:  # one more frame at the first timed seed, gathered, saved by rank 0
-        step(args.seed)
+    if args.dump_frame:
+        # The frame at --seed rendered by the calls the timed steps make (same F, handles and
+        # streams), issued last behind F - 1 other frames still in flight, gathered, saved by
+        # rank 0 as an (H, W, 3) float32 image; tiles no rank rendered (--emulate) are NaN.
+        run_frames([args.seed + 2000 + k for k in range(F - 1)] + [args.seed])
         torch.cuda.synchronize()
         if rank == 0:
-            parts = [g.cpu().numpy() for g in gathered] if dist else [out.cpu().numpy()]
-            np.save(args.dump_frame, tl.unpack(parts, world, n_tiles, T, W, H, deal))
+            if dist:
+                img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H, deal)
+            else:
+                last = fl_out[F - 1] if F > 1 else out
+                img = np.full((H, W, 3), np.nan, dtype=np.float32)
+                buf = last.cpu().numpy().reshape(-1, T, T, 3)
+                for k, tid in enumerate(mine):
+                    x0, y0 = (tid % tiles_x) * T, (tid // tiles_x) * T
+                    w, h = min(T, W - x0), min(T, H - y0)
+                    img[y0:y0 + h, x0:x0 + w] = buf[k, :h, :w]
+            np.save(args.dump_frame, img)
 
     if rank != 0:
         if dist:
@@ -626,6 +708,7 @@ def main():
             **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),
         },
         "roofline": roofline,
+        "ranks": ranks,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -175,7 +175,8 @@ typedef struct rt_render_params {
   uint64_t seed;         /* counter-RNG seed */
   int32_t sync;          /* 1: wait for the render and fill the stats before returning; 0: a one-pass
                             call (rt_stats.path) returns once enqueued on `stream` -- rt_render_wait
-                            (or the scene's next call) finishes it; step-pipeline calls always wait */
+                            (or the scene's next call) finishes it; a step-pipeline or chunked call
+                            completes before returning and rt_render_wait hands out its stats */
   int32_t pad;
 } rt_render_params;
 
@@ -218,8 +219,10 @@ int rt_render_tiles(rt_scene_t scene, const rt_camera_desc* cam, const rt_render
                     const int32_t* tile_ids, int32_t n_tiles, int32_t tile_w, int32_t tile_h,
                     float* d_rgb_out, void* stream, rt_stats* stats);
 
-/* Finishes the scene's deferred call (rt_render_params.sync == 0): waits for it and fills
- * `stats` (may be null); with nothing deferred it returns zeroed stats.  Two scene handles of
+/* Finishes the scene's last call made with rt_render_params.sync == 0: waits for it if it was
+ * deferred (one-pass) and fills `stats` (may be null) -- also when that call had completed
+ * before returning (step pipeline, tile chunks: its stats are held for this wait).  With no such
+ * call outstanding it returns zeroed stats.  Two scene handles of
  * one scene on two streams keep two frames in flight (bench.py --frames-in-flight 2): the
  * next frame's camera rays and the previous frame's shading run in the idle tail of the
  * other frame's trace launch. */

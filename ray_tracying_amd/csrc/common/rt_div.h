@@ -29,3 +29,32 @@ RT_HD inline double rt_div_by(double a, double b, double y) {
   const double r = RT_FMA64(-q0, b, a);
   return RT_FMA64(r, y, q0);
 }
+
+// normalize() (raytracer.cpp:75-79: x / m per component, m = sqrtf(x*x + y*y + z*z)) through
+// one correctly rounded reciprocal and three Markstein quotients where those are RN(x / m):
+// m and 1 / m normal, and every component x with |x| >= 2^-100 and |x| >= m * 2^-120 -- then
+// the remainder x - m * q0 is exact (x at least 2^(emin + 26)) and x / m is normal.  Any other
+// vector -- a zero component (whose sign the correction could lose: -0 / m is -0), a subnormal
+// or tiny one, an extreme length -- takes the three divisions.  tests/test_div.py checks it
+// against the divisions on vectors with zero, signed-zero, subnormal and tiny components.
+RT_HD inline bool rt_quot_by_len_ok(float x, float m) {
+  const float ax = x < 0.0f ? -x : x;
+  return ax >= 0x1p-100f && ax >= m * 0x1p-120f;
+}
+RT_HD inline void rt_normalize3(float& x, float& y, float& z) {
+  const float m = sqrtf(x * x + y * y + z * z);
+  if (m == 0.0f) {
+    x = y = z = 0.0f;
+    return;
+  }
+  if (!(m > 0x1p-120f && m < 0x1p120f) || !(rt_quot_by_len_ok(x, m) && rt_quot_by_len_ok(y, m) && rt_quot_by_len_ok(z, m))) {
+    x = x / m;
+    y = y / m;
+    z = z / m;
+    return;
+  }
+  const float r = 1.0f / m;
+  x = rt_div_by(x, m, r);
+  y = rt_div_by(y, m, r);
+  z = rt_div_by(z, m, r);
+}

@@ -38,15 +38,12 @@ __device__ __forceinline__ V3 normalize(V3 v) {
   if (m == 0.0f) return V3{0.0f, 0.0f, 0.0f};
   return V3{((v.x) / (m)), ((v.y) / (m)), ((v.z) / (m))};
 }
-// normalize() with one correctly rounded reciprocal and three Markstein quotients (rt_div.h):
-// the same bits as three divisions by m while 1 / m stays normal (checked: otherwise the
+// normalize() with one correctly rounded reciprocal and three Markstein quotients where they
+// give the same bits as the three divisions by m (rt_normalize3, rt_div.h; otherwise the
 // divisions themselves)
 __device__ __forceinline__ V3 normalize_rcp(V3 v) {
-  float m = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
-  if (m == 0.0f) return V3{0.0f, 0.0f, 0.0f};
-  if (!(m > 0x1p-120f && m < 0x1p120f)) return V3{((v.x) / (m)), ((v.y) / (m)), ((v.z) / (m))};
-  const float y = 1.0f / m;
-  return V3{rt_div_by(v.x, m, y), rt_div_by(v.y, m, y), rt_div_by(v.z, m, y)};
+  rt_normalize3(v.x, v.y, v.z);
+  return v;
 }
 // std::max / std::min on floats: (a < b) ? b : a  and  (b < a) ? b : a
 __device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }

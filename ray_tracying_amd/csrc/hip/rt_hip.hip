@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -283,7 +284,6 @@ struct TraceArgs {
   int frames, pinhole;
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
-  int drain_leaf_div;         // drain loop: leaf phase once 1/drain_leaf_div of the active lanes wait (0: off)
   int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
   int op_fo, op_ft, op_fk;    // one-pass query fields (LogicArgs): origin, time, kind; -1 absent
   // instrumented one-pass calls: node visits per render-order tile (unit / units per tile),
@@ -648,21 +648,11 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
-#ifdef RT_NODE_SOA
-  // A/B layout (make variant VDEFS=-DRT_NODE_SOA): the node's four 16-B words in four arrays
-  const float4* nd = a.c.nodes + node;
-  const size_t nn = (size_t)a.n_nodes;
-  const float4 g = nd[0];
-  const uint4 qa = *reinterpret_cast<const uint4*>(nd + nn);
-  const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2 * nn);
-  const int4 qc = *reinterpret_cast<const int4*>(nd + 3 * nn);
-#else
   const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
   const float4 g = nd[0];
   const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
   const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
   const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
-#endif
   const uint32_t ex = __float_as_uint(g.w);
   const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
   const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
@@ -1155,11 +1145,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       }
       const uint64_t act = __ballot(item != kNoItem);
       const uint64_t leafm = __ballot(is_leaf_item(item));
-      // the tail is latency-bound: with few lanes left a leaf is tested once 1/drain_leaf_div of
-      // them wait on one, not only when leaf_min do (or nothing else is left)
-      const int nleaf = __popcll(leafm);
-      if (leafm != 0ull && (nleaf >= a.leaf_min || (act & ~leafm) == 0ull ||
-                            (a.drain_leaf_div > 0 && nleaf * a.drain_leaf_div >= __popcll(act)))) {
+      if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
         if (is_leaf_item(item)) {
           const uint32_t e = (uint32_t)item;
           test_prims<kCount, kPlanesOnly, true>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax,
@@ -1274,9 +1260,6 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
 // scattered state loads, so occupancy pays: without frames 4 waves (<= 128 VGPRs; the
 // unconstrained allocation took 132 = 3 waves, 10 % slower frame); with recursion frames
 // the state machine needs ~195 (2 waves).  A/B builds: make variant VDEFS=-DRT_LOGIC_WAVES=5
-#ifndef RT_LOGIC_HIT_AFTER_RES
-#define RT_LOGIC_HIT_AFTER_RES 1  // A/B: 0 loads a closest query's hit record before its result is known
-#endif
 #ifndef RT_LOGIC_WAVES
 #define RT_LOGIC_WAVES 4
 #endif
@@ -1358,7 +1341,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
         mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
         store_hit_pnm(hit_rec(a.hit, slot), hp, hn, (uint32_t)mat_id);
         if (kTex) a.hit_uv[slot] = make_float2(hu, hv);
-      } else if (st0 == ST_SHADOW || (st0 == ST_CLOSEST && (!RT_LOGIC_HIT_AFTER_RES || res_ld >= 0))) {
+      } else if (st0 == ST_SHADOW || (st0 == ST_CLOSEST && res_ld >= 0)) {
         // the hit being shaded: its record (written by the trace kernel for planes-only scenes,
         // by the ST_CLOSEST step above otherwise); a closest miss does not read it
         const HitRec hr = load_hit(hit_rec(a.hit, slot));
@@ -2050,8 +2033,11 @@ template <bool kCount>
 void launch_trace2(const TraceArgs& ta, bool planes, bool soft, unsigned blocks, size_t lds, hipStream_t st) {
   if (ta.n_fuse > 0 && planes)  // point lights only (the host's choice)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
-  else if (ta.n_fuse > 0 || ta.one_pass)  // ... and no textures: the fused path stores no (u, v); one-pass
-                                          // calls of transformed shapes: the lane computes the hit record
+  else if (ta.n_fuse > 0 || (ta.one_pass && !planes))  // ... and no textures: the fused path stores no (u, v);
+                                                       // one-pass calls of transformed shapes: the lane computes
+                                                       // the hit record (planes-only one-pass calls without
+                                                       // lights take the plain planes instance below, whose
+                                                       // finish_query writes a textured hit's (u, v))
     hipLaunchKernelGGL((trace_refill_kernel<kCount, false, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (soft && planes)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
@@ -2186,12 +2172,11 @@ struct rt_scene_s {
   std::vector<float> cost_pts;
   std::vector<unsigned char> cost_key;
   std::vector<float> tile_cost;
-  // measured tile costs (one-pass calls): lane node visits per tile id of the last calls with
-  // this camera / tile size / sample count (-1: not measured yet), and their device / pinned
-  // host counters
+  // measured tile costs (instrumented one-pass calls, rt_tile_costs_measured): lane node visits
+  // per tile id of the last calls with this camera / tile size / sample count (-1: not measured
+  // yet), and their device / pinned host counters
   std::vector<unsigned char> meas_key;
-  std::vector<float> meas_cost;    // the order key: node visits per ray of the tile (RT_MEASURED_ORDER=2: total)
-  std::vector<float> meas_visits;  // node visits of the tile
+  std::vector<float> meas_visits;
   unsigned int* d_tile_cost = nullptr;
   unsigned int* h_tile_cost = nullptr;
   size_t cap_tile_cost = 0, cap_h_tile_cost = 0;
@@ -2206,6 +2191,10 @@ struct rt_scene_s {
     TraceArgs ta{};
 #endif
   } pending;
+  // a call with rt_render_params.sync == 0 that completed before returning (the step pipeline,
+  // or a call split into tile chunks): its statistics, handed out by the next rt_render_wait
+  bool held = false;
+  rt_stats held_stats{};
   int fuse_lights = 0;  // > 0: point lights whose shadow rays the trace kernel may fuse (see rt_scene_create)
 };
 
@@ -2278,26 +2267,15 @@ static std::vector<unsigned char> meas_key_of(const rt_camera_desc* cam, int til
   return key;
 }
 
-// Tiles with a measured cost (an earlier instrumented one-pass call -- count_work -- of this
-// camera / tile size / sample count: its trace kernel's node visits per tile) are ordered by it -- it sees what the
-// projected-centre estimate misses, the rays that graze the object's silhouette and cross
-// much of it; the others by the estimate.
+// Tiles are ordered by the projected-centre estimate (ordering by the node visits an
+// instrumented call measured per tile was 4 % slower on one rank's eighth, r04: those
+// measurements serve bench.py's `--deal measured` instead).
 static void tile_cost_order(rt_scene_s* s, const rt_camera_desc* cam, int tile_w, int tile_h, int tiles_x, int tiles_y,
-                            int n_samples, const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
+                            const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
   order.resize((size_t)n_tiles);
   for (int i = 0; i < n_tiles; ++i) order[i] = i;
   if (const char* e = std::getenv("RT_TILE_ORDER")) wanted = std::atoi(e) != 0;  // 0 / 1: never / always
   if (!wanted || n_tiles < 2) return;
-  bool measured = false;  // RT_MEASURED_ORDER=1 / 2: by measured cost per ray / total (A/B; the estimate by default)
-  if (const char* e = std::getenv("RT_MEASURED_ORDER"))
-    measured = std::atoi(e) != 0 && s->meas_key == meas_key_of(cam, tile_w, tile_h, n_samples);
-  for (int i = 0; i < n_tiles && measured; ++i) measured = s->meas_cost[(size_t)tile_ids[i]] >= 0.0f;
-  if (measured) {
-    std::stable_sort(order.begin(), order.end(), [&](int i, int j) {
-      return s->meas_cost[(size_t)tile_ids[i]] > s->meas_cost[(size_t)tile_ids[j]];
-    });
-    return;
-  }
   if (s->cost_pts.empty()) return;
   const std::vector<float>& cost = tile_costs(s, cam, tile_w, tile_h, tiles_x, tiles_y);
   std::stable_sort(order.begin(), order.end(), [&](int i, int j) {
@@ -2334,17 +2312,10 @@ static int upload(void** dst, const void* src, size_t bytes) {
   return RT_OK;
 }
 
-// The 64-B nodes as laid out in HBM: AoS (one node = four consecutive 16-B words, fetched by
-// one lane), or -- the RT_NODE_SOA A/B build -- word k of every node in array k.
+// The 64-B nodes as laid out in HBM: AoS, one node = four consecutive 16-B words fetched by
+// one lane (an SoA layout -- word k of every node in array k -- measured 2.3 % slower, r04).
 static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
-#ifdef RT_NODE_SOA
-  std::vector<float4> t((size_t)n * 4);
-  for (int32_t i = 0; i < n; ++i)
-    for (int k = 0; k < 4; ++k) std::memcpy(&t[(size_t)k * n + i], reinterpret_cast<const char*>(&nodes[i]) + 16 * k, 16);
-  return upload(dst, t.data(), t.size() * sizeof(float4));
-#else
   return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
-#endif
 }
 
 int rt_scene_destroy(rt_scene_t s) {
@@ -2561,16 +2532,9 @@ static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
   if (q.measure_tiles) {  // measured tile costs, by tile id (render-order index i holds tile tl_dev[i])
     if (s->meas_key != q.meas_key) {
       s->meas_key = q.meas_key;
-      s->meas_cost.assign((size_t)q.tiles_x * q.tiles_y, -1.0f);
       s->meas_visits.assign((size_t)q.tiles_x * q.tiles_y, -1.0f);
     }
-    // RT_MEASURED_ORDER=2: total node visits; otherwise node visits per ray (a tile's mean ray cost)
-    const bool total = std::getenv("RT_MEASURED_ORDER") && std::atoi(std::getenv("RT_MEASURED_ORDER")) == 2;
-    for (int i = 0; i < q.n_tiles; ++i) {
-      const float v = (float)s->h_tile_cost[2 * i], r = (float)s->h_tile_cost[2 * i + 1];
-      s->meas_cost[(size_t)q.tl_dev[i]] = total ? v : (r > 0.0f ? v / r : 0.0f);
-      s->meas_visits[(size_t)q.tl_dev[i]] = v;
-    }
+    for (int i = 0; i < q.n_tiles; ++i) s->meas_visits[(size_t)q.tl_dev[i]] = (float)s->h_tile_cost[2 * i];
   }
   float ms = 0.f, t_a = 0.f, t_b = 0.f, k_ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[0][0], s->ev_b[0][0]), RT_EDEVICE);
@@ -2609,9 +2573,10 @@ static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
 // slot state.  The scene must need nothing between a sample's camera ray and its colour but the
 // closest hit and one shadow ray per light, traced by the tracing lane: no Trace recursion
 // (reflection / refraction), lights all points (the fused shadow rays: at most 24) or none,
-// and the hit's (u, v) from the trace kernel (planes) or no texture.  RT_ONE_PASS=0 turns it
-// off; an explicit RT_SLOTS / RT_PIPES / RT_FUSE (the step pipeline's knobs) or a diagnostic mode that
-// waits on every step (RT_DIAG, RT_TRACE_REPLAY) selects the step pipeline too.
+// and the hit's (u, v) from the trace kernel (planes) or no texture.  RT_ONE_PASS=0 selects the
+// step pipeline for every call, and nothing else does: the step pipeline's own knobs (RT_SLOTS,
+// RT_PIPES, RT_FUSE) and its per-step log (RT_DIAG) do not apply to a one-pass call, which ignores
+// them and says so once per process (note_ignored_knobs).
 static bool one_pass_scene(const rt_scene_s* s) {
   const bool frames = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
   const bool tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
@@ -2620,8 +2585,15 @@ static bool one_pass_scene(const rt_scene_s* s) {
 }
 static bool one_pass_env() {
   if (const char* e = std::getenv("RT_ONE_PASS")) return std::atoi(e) != 0;
-  return !std::getenv("RT_SLOTS") && !std::getenv("RT_PIPES") && !std::getenv("RT_FUSE") && !std::getenv("RT_DIAG") &&
-         !std::getenv("RT_TRACE_REPLAY");
+  return true;
+}
+static void note_ignored_knobs() {
+  static std::atomic<bool> said[4] = {};
+  static const char* const knobs[4] = {"RT_SLOTS", "RT_PIPES", "RT_FUSE", "RT_DIAG"};
+  for (int k = 0; k < 4; ++k)
+    if (std::getenv(knobs[k]) && !said[k].exchange(true))
+      std::fprintf(stderr, "librt_hip: %s applies to the step pipeline only; one-pass calls ignore it "
+                   "(RT_ONE_PASS=0 selects the step pipeline)\n", knobs[k]);
 }
 // units of one one-pass call (larger calls run as tile chunks): 52 B of workspace per unit
 // touched (query direction 12, result 4, hit record 32 on a hit, occlusion bits 4)
@@ -2635,6 +2607,11 @@ extern "C" {
 
 int rt_render_wait(rt_scene_t s, rt_stats* stats) {
   if (!s) return fail(RT_EINVAL, "rt_render_wait: null scene");
+  if (!s->pending.active && s->held) {  // a sync == 0 call that had completed already
+    s->held = false;
+    if (stats) *stats = s->held_stats;
+    return RT_OK;
+  }
   return finish_one_pass(s, stats);
 }
 
@@ -2650,9 +2627,35 @@ int rt_tile_costs_measured(rt_scene_t s, const rt_camera_desc* cam, int32_t tile
   return RT_OK;
 }
 
+}  // extern "C"
+
+static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
+                        int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr, rt_stats* stats);
+
+extern "C" {
+
+// A call with sync == 0 is finished by rt_render_wait, whichever path ran: a deferred one-pass
+// call is waited for there; a call that completed before returning (the step pipeline, tile
+// chunks) leaves its statistics for it (held), so the caller's wait never reads zeros.
 int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
                     int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
                     rt_stats* stats) {
+  if (s) s->held = false;
+  rt_stats st{};
+  const int rc = render_tiles(s, cam, p, tile_ids, n_tiles, tile_w, tile_h, d_out, stream_ptr, &st);
+  if (rc == RT_OK && p->sync == 0 && !s->pending.active) {
+    s->held = true;
+    s->held_stats = st;
+  }
+  if (stats) *stats = st;
+  return rc;
+}
+
+}  // extern "C"
+
+static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
+                        int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
+                        rt_stats* stats) {
   if (!s || !cam || !p || (!tile_ids && n_tiles > 0) || !d_out) return fail(RT_EINVAL, "rt_render_tiles: null argument");
   if (tile_w <= 0 || tile_h <= 0 || tile_w % 8 || tile_h % 8)
     return fail(RT_EINVAL, "rt_render_tiles: tile size must be a positive multiple of 8");
@@ -2681,8 +2684,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
       pc.sync = 1;  // chunks share the workspace: each one finishes before the next
       for (int t0 = 0; t0 < n_tiles; t0 += k) {
         rt_stats st{};
-        const int rc = rt_render_tiles(s, cam, &pc, tile_ids + t0, std::min(k, n_tiles - t0), tile_w, tile_h,
-                                       d_out + (size_t)t0 * tile_w * tile_h * 3, stream_ptr, &st);
+        const int rc = render_tiles(s, cam, &pc, tile_ids + t0, std::min(k, n_tiles - t0), tile_w, tile_h,
+                                    d_out + (size_t)t0 * tile_w * tile_h * 3, stream_ptr, &st);
         if (rc) return rc;
         acc.rays += st.rays;
         acc.box_tests += st.box_tests;
@@ -2721,6 +2724,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   const bool frames_scene = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
   const bool tex_scene = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   const bool one_pass = one_pass_scene(s) && one_pass_env() && n_units <= one_pass_cap();
+  if (one_pass) note_ignored_knobs();
   long long slots = frames_scene ? std::min(n_units, 16LL << 20) : std::min(n_units, 128LL << 20);
   if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
   // slot-state words are addressed S[field * N + slot] in 32-bit int: (highest field + 1) * N
@@ -2775,7 +2779,7 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // 4509-4564 -> 4723-4727 Mrays/s.  Longer calls keep the caller's order (whole frames,
   // C4, C5: within -1.6 %..+0 % -- the other pipeline hides their drains).
   std::vector<int32_t> order;
-  tile_cost_order(s, cam, tile_w, tile_h, tiles_x, tiles_y, n_samples, tile_ids, n_tiles, n_units <= n_slots, order);
+  tile_cost_order(s, cam, tile_w, tile_h, tiles_x, tiles_y, tile_ids, n_tiles, n_units <= n_slots, order);
   std::vector<int32_t> tl_dev((size_t)n_tiles * 2);
   bool identity = true;
   for (int i = 0; i < n_tiles; ++i) {
@@ -2884,8 +2888,6 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // are the serial near-first traversal's (the algorithmic bytes bench.py reports)
   ta.drain_help = p->count_work ? 0 : 1;
   if (const char* e = std::getenv("RT_DRAIN_HELP")) ta.drain_help = std::atoi(e) != 0 ? 1 : 0;
-  ta.drain_leaf_div = 0;
-  if (const char* e = std::getenv("RT_DRAIN_LEAF_DIV")) ta.drain_leaf_div = std::max(0, std::min(64, std::atoi(e)));
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
   for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
@@ -2903,7 +2905,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // camera and shadow rays interleave within a wave and lose coherence (headline -6.5 %).
   // RT_FUSE=0 / 1 overrides (1: whenever the scene allows it).
   ta.n_fuse = n_units <= 2LL * n_slots || s->desc.n_prims < kFuseFewPrims ? s->fuse_lights : 0;
-  if (const char* e = std::getenv("RT_FUSE")) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
+  if (const char* e = std::getenv("RT_FUSE"))  // (a one-pass call traces every point light's shadow ray fused)
+    if (!one_pass) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
   // the launched instance (launch_trace2): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
   // entries except fused shadows over transformed shapes (5, 16)
   ta.one_pass = one_pass ? 1 : 0;
@@ -2937,16 +2940,13 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   // entry + t_near per stack slot
   const size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
 
-  int replay_iter = -1, replay_reps = 0;
   const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
   const bool steps_log = std::getenv("RT_STEPS_LOG") != nullptr;  // diagnostic: every trace launch, any pipeline
-  if (const char* e = std::getenv("RT_TRACE_REPLAY")) std::sscanf(e, "%d:%d", &replay_iter, &replay_reps);
-  if (soft_trace) replay_iter = -1;  // a replay would draw the soft-light samples again from advanced state
   // the diagnostics wait on every step (one pipeline)
 #ifdef RT_EXIT_TIMING
   const bool step_sync = true;
 #else
-  const bool step_sync = diag || replay_iter >= 0;
+  const bool step_sync = diag;
 #endif
 
   // ---- pipelines: the slots may split into independent logic -> trace sequences, one per
@@ -3166,29 +3166,6 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
         if (stats && hipEventElapsedTime(&t_a, s->ev_t0, s->ev_a[h][k]) == hipSuccess &&
             hipEventElapsedTime(&t_b, s->ev_t0, s->ev_b[h][k]) == hipSuccess)
           busy.emplace_back(t_a, t_b);
-        if (replay_iter == iters && replay_reps > 0 && !p->count_work) {  // one pipeline, batch == 1 here
-          // diagnostic (RT_TRACE_REPLAY=iter:reps): re-trace this step's queries; the results
-          // are recomputed identically, so the frame is unchanged
-          float tot = 0.f, best = 1e30f;
-          unsigned long long rays0 = 0;
-          HIP_TRY(hipMemcpy(&rays0, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-          for (int r = 0; r < replay_reps; ++r) {
-            HIP_TRY(hipMemsetAsync(P.ta.fetch, 0, (size_t)ta.fetch_shards * kFetchStride * 4, stream), RT_EDEVICE);
-            HIP_TRY(hipEventRecord(s->ev_a[0][1], stream), RT_EDEVICE);
-            launch_trace(P.ta, false, planes_only, soft_trace, P.trace_blocks, lds, stream);
-            HIP_TRY(hipEventRecord(s->ev_b[0][1], stream), RT_EDEVICE);
-            HIP_TRY(hipEventSynchronize(s->ev_b[0][1]), RT_EDEVICE);
-            float m = 0.f;
-            HIP_TRY(hipEventElapsedTime(&m, s->ev_a[0][1], s->ev_b[0][1]), RT_EDEVICE);
-            tot += m;
-            best = std::min(best, m);
-          }
-          unsigned long long rays1 = 0;
-          HIP_TRY(hipMemcpy(&rays1, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-          HIP_TRY(hipMemcpy(ctl + 8, &rays0, 8, hipMemcpyHostToDevice), RT_EDEVICE);  // keep the frame's ray count
-          std::fprintf(stderr, "[rt replay] step %d: %llu queries, trace %.4f ms avg / %.4f ms min over %d reps\n", iters,
-                       (rays1 - rays0) / (unsigned long long)replay_reps, tot / replay_reps, best, replay_reps);
-        }
         const bool more = flag[(size_t)k * kFetchStride] != 0;
 #ifdef RT_EXIT_TIMING
         if (more) print_exit_log(P.ta, ms, iters);
@@ -3271,6 +3248,8 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   }
   return RT_OK;
 }
+
+extern "C" {
 
 int rt_malloc(int32_t device, size_t bytes, void** d_ptr) {
   if (!d_ptr) return fail(RT_EINVAL, "rt_malloc: null");

@@ -4,6 +4,9 @@
 //   div_check f32 sweep B E0 E1        every binary32 a in [2^E0, 2^E1) against divisor B
 //   div_check f64 random N SEED
 //   div_check f64 jitter S N SEED      a = si + U[0,1) (the stratified jitter), divisor S
+//   div_check f32 norm N SEED          rt_normalize3 against three divisions by the length, on
+//                                      vectors mixing normal, zero, -0, subnormal, tiny and huge
+//                                      components (bit patterns compared: the sign of a zero counts)
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -56,6 +59,37 @@ int main(int argc, char** argv) {
       memcpy(&a, &u, 4);
       volatile float va = a, vb = b;
       if (rt_div_by((float)va, (float)vb, y) != va / vb) ++bad;
+      ++checked;
+    }
+  } else if (!strcmp(argv[2], "norm")) {
+    const long long n = atoll(argv[3]);
+    std::mt19937_64 g(strtoull(argv[4], 0, 10));
+    auto comp = [&]() -> float {
+      const unsigned k = (unsigned)(g() % 8);
+      const bool neg = g() & 1;
+      float v;
+      if (k == 0) v = 0.0f;
+      else if (k == 1) {  // subnormal
+        const uint32_t u = 1u + (uint32_t)(g() % 0x7fffffu);
+        memcpy(&v, &u, 4);
+      } else if (k == 2) v = std::ldexp(1.0f + (float)(g() >> 40) * 0x1p-24f, -126 + (int)(g() % 40));  // tiny normal
+      else if (k == 3) v = std::ldexp(1.0f + (float)(g() >> 40) * 0x1p-24f, 40 + (int)(g() % 88));     // huge
+      else v = std::ldexp(1.0f + (float)(g() >> 40) * 0x1p-24f, -8 + (int)(g() % 12));                // camera-like
+      return neg ? -v : v;
+    };
+    for (long long i = 0; i < n; ++i) {
+      volatile float x = comp(), y = comp(), z = comp();
+      float a = x, b = y, c = z;
+      rt_normalize3(a, b, c);
+      const float m = sqrtf(x * x + y * y + z * z);
+      float r[3] = {0.0f, 0.0f, 0.0f};
+      if (m != 0.0f) {
+        r[0] = x / m;
+        r[1] = y / m;
+        r[2] = z / m;
+      }
+      const float q[3] = {a, b, c};
+      if (memcmp(q, r, sizeof q) != 0) ++bad;
       ++checked;
     }
   } else if (!strcmp(argv[2], "jitter")) {

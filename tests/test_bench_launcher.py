@@ -47,6 +47,16 @@ def test_gpus_flag_spawns_ranks(n):
     assert len(lines) == 1, r.stdout  # rank 0 alone prints
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["ranks_in_group"] == n
+    # the per-rank summary rank 0 prints (all-gathered over the ranks' process group): every rank's
+    # wall / render / gather time per step and rays, and which rank was slowest (the dry run's
+    # stand-in timings give rank r r + 1 ms of render per step)
+    rk = d["ranks"]
+    assert rk["n"] == n
+    for key in ("wall_ms_per_step", "render_ms_per_step", "gather_ms_per_step", "rays_per_step"):
+        assert len(rk[key]) == n, key
+    assert rk["render_ms_per_step"] == [float(r + 1) for r in range(n)]
+    assert rk["slowest_rank"] == n - 1 and rk["slowest_render_ms_per_step"] == float(n)
+    assert rk["fastest_render_ms_per_step"] == 1.0
 
 
 def test_world_size_mismatch_fails():

@@ -49,3 +49,11 @@ def test_div_jitter_f64(checker, s):
 def test_div_sweep_f32(checker, b):
     checked, bad = run(checker, "f32", "sweep", b, -1, 13)  # px in [0.5, 8192): every binary32 value
     assert checked == 14 * 2 ** 23 and bad == 0
+
+
+def test_normalize_rcp_f32(checker):
+    """rt_normalize3 (the camera's normalize_rcp) == three divisions by the length, bit for bit,
+    including vectors with zero, -0, subnormal, tiny and huge components (the
+    Markstein quotient needs a normal numerator and quotient; such vectors take the divisions)."""
+    checked, bad = run(checker, "f32", "norm", 5_000_000, 3)
+    assert checked == 5_000_000 and bad == 0

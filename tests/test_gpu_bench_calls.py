@@ -1,0 +1,118 @@
+"""Parity of the exact calls bench.py times.
+
+The other full-scale parity tests render a few tiles per call.  The timed calls differ: the
+headline step is one one-pass call over all 256 tiles of the 1024^2 x 100 spp frame (104.9M
+units, costliest tiles first, their outputs remapped to the caller's order); C5 is one call of
+2^30 units over the whole 4096^2 x 64 spp frame (64-bit query offsets, ~56 GB of workspace);
+a rank's share of an 8-way split is rendered with two frames in flight, deferred, on two scene
+handles and streams.  Each test runs bench.py itself (`--dump-frame`: after the timed steps the
+frame at --seed is rendered by the same calls -- same frames in flight, issued behind another
+frame still in flight -- and saved) and compares it with the oracle (counter RNG) bit for bit:
+the whole headline frame and the whole rank share, with equal ray counts (the timed frame with
+--steps 1 is the frame at --seed: config.rays_per_step); for C5 a spread of tiles (the whole
+frame is ~1.5G rays, hours for the CPU restatement), so its ray count is not compared.
+
+The loop these calls replace: /root/reference/Code/raytracer.cpp:433-476 (compute_pixel_color
+per pixel, :18-70); the traversal: Code/acceleration.cpp:67-118.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+import ray_tracying_amd as rt
+from ray_tracying_amd import tiles as tl
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SEED = 20251226  # bench.py's --seed and soup seed
+T = 64
+
+
+def _soup(tmp_path_factory, res):
+    p = str(tmp_path_factory.mktemp(f"soup{res}") / "soup1m.json")
+    rt.make_soup(p, 1_000_000, seed=SEED, width=res, height=res)
+    return p
+
+
+@pytest.fixture(scope="module")
+def soup1024(tmp_path_factory):
+    return _soup(tmp_path_factory, 1024)
+
+
+def _bench(tmp_path, tag, *args):
+    frame = str(tmp_path / f"{tag}.npy")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--pmc-traffic", "",
+           "--pmc-valu", "", "--dump-frame", frame, *args]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    return np.load(frame), line
+
+
+def _compare(img, path, res, spp_sqrt, tiles):
+    tiles_x = res // T
+    regions = [((t % tiles_x) * T, (t // tiles_x) * T, T, T) for t in tiles]
+    ref, ost = ob.render_regions(path, regions, use_bvh=True, spp_sqrt=spp_sqrt, light_samples=1, seed=SEED,
+                                 resolution=(res, res))
+    for k, t in enumerate(tiles):
+        x0, y0 = (t % tiles_x) * T, (t // tiles_x) * T
+        got = np.ascontiguousarray(img[y0:y0 + T, x0:x0 + T])
+        bad = int((got.view(np.uint32) != ref[k].view(np.uint32)).sum())
+        assert bad == 0, f"tile {t}: {bad} channels differ from the oracle"
+    return ost["rays"]
+
+
+def test_headline_frame_as_timed(soup1024, tmp_path, gpu):
+    """bench.py's default step: the whole 1024^2 x 100 spp frame in one one-pass call."""
+    img, line = _bench(tmp_path, "head")
+    assert line["config"]["frames_in_flight"] == 1 and line["config"]["pipeline"].startswith("one-pass")
+    assert np.isfinite(img).all()
+    rays = _compare(img, soup1024, 1024, 10, list(range(16 * 16)))
+    assert rays == line["config"]["rays_per_step"]
+
+
+def test_rank_share_as_timed(soup1024, tmp_path, gpu):
+    """One rank's share of the 8-way split (rank 7: 32 tiles of the lattice deal) rendered as its
+    rank does: two frames in flight, deferred, on two scene handles and streams."""
+    img, line = _bench(tmp_path, "em8", "--emulate", "8", "--emulate-rank", "7")
+    assert line["config"]["frames_in_flight"] == 2
+    mine = [int(t) for t in tl.assign_tiles(256, 8, 7, 16)]
+    assert len(mine) == 32
+    done = np.isfinite(img).all(axis=2)
+    for t in range(256):  # exactly the share's tiles were rendered
+        assert bool(done[(t // 16) * T, (t % 16) * T]) == (t in mine), t
+    rays = _compare(img, soup1024, 1024, 10, mine)
+    assert rays == line["config"]["rays_per_step"]
+
+
+def test_c5_frame_as_timed(tmp_path_factory, tmp_path, gpu):
+    """C5 as timed: the whole 4096^2 x 64 spp frame (2^30 units) in one one-pass call; tiles at
+    the centre, the corners, the edges and across the soup's silhouette (64 x 64 tile grid)."""
+    path = _soup(tmp_path_factory, 4096)
+    img, line = _bench(tmp_path, "c5", "--res", "4096", "--spp-sqrt", "8")
+    assert line["config"]["pipeline"].startswith("one-pass") and line["config"]["resolution"] == "4096x4096"
+    assert np.isfinite(img).all()
+    tiles = [32 * 64 + 32, 0, 63, 63 * 64, 63 * 64 + 63, 32 * 64 + 11, 32 * 64 + 52, 11 * 64 + 32, 52 * 64 + 20,
+             44 * 64 + 47]
+    _compare(img, path, 4096, 8, tiles)
+
+
+def test_step_pipeline_scene_frames_in_flight(tmp_path, gpu):
+    """frames in flight on a step-pipeline scene (C4's glossy reflection with soft
+    lights).  Its calls complete before returning, so by default bench.py keeps one frame in
+    flight; forced to two, every frame's statistics still reach the line (DeviceScene.wait hands
+    out the held stats) -- never a silent 0 Mrays/s -- and the frame is the same."""
+    scene = os.path.join(ROOT, "tests", "golden", "scenes", "blend", "glossy_reflection.json")
+    common = ("--scene", scene, "--res", "128", "--spp-sqrt", "2", "--light-radius", "1.0", "--light-samples", "2")
+    auto_img, auto = _bench(tmp_path, "c4auto", *common)
+    assert auto["config"]["frames_in_flight"] == 1 and auto["config"]["pipeline"].startswith("steps")
+    two_img, two = _bench(tmp_path, "c4two", *common, "--frames-in-flight", "2")
+    assert two["config"]["frames_in_flight"] == 2
+    assert two["value"] > 0 and two["config"]["rays_per_step"] == auto["config"]["rays_per_step"] > 0
+    assert int((auto_img.view(np.uint32) != two_img.view(np.uint32)).sum()) == 0

@@ -7,8 +7,9 @@ lane continues soft-shadow samples (kSoft, soft_start) and reflection chains go 
 renders four 64x64 tiles of the frame through rt_render_tiles -- the call bench.py times --
 chosen to cover the spheres, the cube, the floor and their reflections; the oracle renders
 the same regions in counter-RNG mode.  Bar: every float bit-identical and the ray counts
-equal, with the default single slot pipeline and with two (RT_PIPES=2, which an explicit
-request allows at any call size: the multi-pipeline scheduler at the full configurations).
+equal, by default (C3 one-pass, C4 the step pipeline) and through the step pipeline with two
+slot pipelines (RT_ONE_PASS=0 RT_PIPES=2, which an explicit request allows at any call size:
+the multi-pipeline scheduler at the full configurations).
 """
 import os
 
@@ -51,7 +52,7 @@ def _check(path, tiles, spp_sqrt, light_samples, seed):
                                  seed=seed, texture_root=scenes.TEXTURES, resolution=(RES, RES))
     sc = rt.Scene(path, resolution=(RES, RES), texture_root=scenes.TEXTURES)
     try:
-        for env in ({}, {"RT_PIPES": "2"}):
+        for env in ({}, {"RT_ONE_PASS": "0", "RT_PIPES": "2"}):
             img, st = _render(sc, tiles, spp_sqrt, light_samples, seed, env)
             for i, t in enumerate(tiles):
                 bad = int((img[i].view(np.uint32) != ref[i].view(np.uint32)).sum())

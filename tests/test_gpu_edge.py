@@ -115,6 +115,7 @@ def test_lockstep_batches_past_the_image_edge(tmp_path, gpu, monkeypatch):
     of the 64-pixel tile, some steps claim only batches whose pixels all lie outside the image
     (the right edge tile's padding columns).  Such a claim must still keep the frame going --
     no batch may be left unclaimed and no pixel read from stale samples."""
+    monkeypatch.setenv("RT_ONE_PASS", "0")  # the step pipeline (this soup is one-pass otherwise)
     monkeypatch.setenv("RT_SLOTS", "4096")
     monkeypatch.setenv("RT_PIPES", "1")
     p = scenes.write(scenes.soup(600, seed=3, res=(72, 40), light=False), str(tmp_path / "s.json"))

@@ -4,7 +4,8 @@ lights' shadow rays right after it and leaves occlusion bits for the logic step.
 oracle bit for bit (and in ray count): with reflection, refraction and glossy fuzz after the
 shade (raytracer.cpp:180-350), in BVH and linear modes, and with 24 lights (the last bit of the
 occlusion word).  RT_FUSE is read per call, so each setting renders in a child process like
-the other knobs (tests/test_gpu_knobs.py)."""
+the other knobs (tests/test_gpu_knobs.py); RT_ONE_PASS=0 keeps the point-lit planes scenes,
+one-pass otherwise (tests/test_gpu_one_pass.py), on the step pipeline whose fusion this tests."""
 import os
 import subprocess
 import sys
@@ -33,7 +34,8 @@ print(st.rays)
 
 def render_child(path, out, spp, bvh, fuse, light_samples=1, env=None):
     r = subprocess.run([sys.executable, "-c", CHILD, ROOT, path, out, str(spp), "1" if bvh else "0", str(light_samples),
-                        scenes.TEXTURES], env={**os.environ, "RT_FUSE": fuse, **(env or {})}, capture_output=True,
+                        scenes.TEXTURES], env={**os.environ, "RT_ONE_PASS": "0", "RT_FUSE": fuse, **(env or {})},
+                       capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     return np.load(out), int(r.stdout.strip().splitlines()[-1])

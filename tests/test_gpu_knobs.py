@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 
 import oracle_bind as ob
+import ray_tracying_amd as rt
 import scenes
 
 pytestmark = pytest.mark.gpu
@@ -32,28 +33,37 @@ import ray_tracying_amd as rt
 sc = rt.Scene(sys.argv[2], texture_root=sys.argv[4])
 img, st = sc.render(rt.RenderParams(spp_sqrt=2, light_samples=2, use_bvh=True, seed=5))
 np.save(sys.argv[3], img)
+print(st.path)
 print(st.rays)
 """
 
+# RT_ONE_PASS=0 runs one-pass scenes (the soup) through the step pipeline, whose knobs the
+# entries below exercise; without it a one-pass call ignores the step pipeline's knobs (last
+# entries: it must stay one-pass and bit-exact -- VERDICT r04 item 7)
+STEPS = {"RT_ONE_PASS": "0"}
 KNOBS = [
     {"RT_LDS_STACK": "2"},
     {"RT_LEAF_MIN": "1", "RT_REFILL": "64"},
     {"RT_LEAF_MIN": "64", "RT_REFILL": "1"},
-    {"RT_BATCH_SHARDS": "1", "RT_FETCH_SHARDS": "64", "RT_SLOTS": "4096"},
+    {"RT_BATCH_SHARDS": "1", "RT_FETCH_SHARDS": "64", "RT_SLOTS": "4096", **STEPS},
     {"RT_BATCH_SHARDS": "1024", "RT_FETCH_SHARDS": "1"},
-    {"RT_BATCH_SHARDS": "1024", "RT_SLOTS": "4096"},  # more shards than slot-waves: clamped
+    {"RT_BATCH_SHARDS": "1024", "RT_SLOTS": "4096", **STEPS},  # more shards than slot-waves: clamped
     {"RT_MAX_UNITS": "3000"},  # the call runs as many tile chunks
-    {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64"},
+    {"RT_PIPES": "2", "RT_SLOTS": "4096", "RT_BATCH_SHARDS": "64", **STEPS},
     {"RT_SOFT_START": "0"},  # a closest hit's first shadow sample emitted by the logic step
     {"RT_SOFT_FUSE": "0"},  # soft-shadow samples advanced by shadow_step_kernel, not the tracing lane
     {"RT_SOFT_FUSE": "0", "RT_SHADOW_STEP": "0"},  # ... or by the logic kernel itself
     {"RT_COLLAPSE": "greedy"},  # the round-1 BVH2 -> BVH4 collapse instead of the SAH-optimal one
-    {"RT_FUSE": "0"},  # point-light shadow rays as their own queries (small calls fuse them by default)
-    {"RT_PIPES": "2"},  # two slot pipelines on two streams (the default is one)
+    {"RT_FUSE": "0", **STEPS},  # point-light shadow rays as their own queries (small calls fuse them by default)
+    {"RT_PIPES": "2", **STEPS},  # two slot pipelines on two streams (the default is one)
     {"RT_TILE_ORDER": "0"},  # tiles in the caller's order (small calls render costliest tiles first)
-    {"RT_PIPES": "4", "RT_SLOTS": "8192"},  # four pipelines of two slot blocks each
+    {"RT_PIPES": "4", "RT_SLOTS": "8192", **STEPS},  # four pipelines of two slot blocks each
     {"RT_DRAIN_HELP": "0"},  # no drain helpers: each query traversed by its own lane alone
     {"RT_DRAIN_HELP": "1", "RT_LDS_STACK": "2", "RT_LEAF_MIN": "1"},  # helpers take entries from the HBM spill area
+    {"RT_DRAIN_HELP": "0", **STEPS},  # the step pipeline without helpers
+    # step-pipeline knobs on a one-pass scene: ignored (one message each), still one-pass
+    {"RT_FUSE": "1"},
+    {"RT_FUSE": "0", "RT_SLOTS": "4096", "RT_PIPES": "2", "RT_DIAG": "1"},
 ]
 
 
@@ -73,4 +83,11 @@ def test_knobs_do_not_change_results(scene, tmp_path, gpu):
         img = np.load(out)
         diff = int((img.view(np.uint32) != ref.view(np.uint32)).sum())
         assert diff == 0, f"{env}: {diff} channels differ"
-        assert int(r.stdout.strip().splitlines()[-1]) == ost["rays"], env
+        path, rays = map(int, r.stdout.strip().splitlines()[-2:])
+        assert rays == ost["rays"], env
+        one_pass_scene = scene == "soup"  # features: reflection, refraction, soft lights -> steps
+        assert path == (rt.PATH_ONE_PASS if one_pass_scene and "RT_ONE_PASS" not in env else rt.PATH_STEPS), env
+        if one_pass_scene and "RT_ONE_PASS" not in env:  # an ignored knob says so once
+            for k in ("RT_SLOTS", "RT_PIPES", "RT_FUSE", "RT_DIAG"):
+                if k in env:
+                    assert f"librt_hip: {k} applies to the step pipeline only" in r.stderr, (env, k)

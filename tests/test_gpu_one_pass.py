@@ -50,6 +50,14 @@ def _textured_soup():
     return sc
 
 
+def _textured_dark_soup():
+    """Textured planes and no lights: the one-pass call takes the plain planes
+    trace instance, whose finish_query writes each textured hit's (u, v) for the shading."""
+    sc = _textured_soup()
+    sc["lights"] = []
+    return sc
+
+
 def _multi_light_soup():
     sc = scenes.soup(2000, seed=8, res=(48, 40))
     sc["lights"] += [{"location": [-2.0, -2.5, 1.0], "intensity": 300.0, "color": [0.4, 0.6, 1.0], "radius": 0.0},
@@ -62,6 +70,7 @@ CASES = {
     "soup_dark": (lambda: scenes.soup(3000, seed=12, res=(64, 64), light=False), 1),
     "soup_degenerate": (lambda: scenes.soup_degenerate(res=(48, 40)), 2),
     "soup_textured": (_textured_soup, 2),
+    "soup_textured_dark": (_textured_dark_soup, 2),
     "soup_three_lights": (_multi_light_soup, 2),
     "shapes_lit": (lambda: _flat(scenes.features(res=(136, 72))), 2),
     "shapes_dark": (lambda: {**_flat(scenes.features(res=(40, 32))), "lights": []}, 1),
@@ -159,4 +168,31 @@ def test_deferred_frames_in_flight(tmp_path, gpu):
     finally:
         for h in hs:
             h.close()
+        sc.close()
+
+
+def test_deferred_call_on_the_step_pipeline(tmp_path, gpu):
+    """a sync=False call that runs the step pipeline (reflection, refraction, soft
+    lights) -- or as tile chunks -- completes before returning; DeviceScene.wait() must still
+    hand out its statistics (once), equal to the synchronous call's, not zeros."""
+    import torch
+    path = scenes.write(scenes.features(res=(64, 48)), str(tmp_path / "f.json"))
+    sc = rt.Scene(path, texture_root=scenes.TEXTURES)
+    ds = rt.DeviceScene(sc, 0)
+    try:
+        T = 32
+        ids = np.arange(2 * 2, dtype=np.int32)
+        a = torch.zeros(ids.size * T * T * 3, dtype=torch.float32, device="cuda:0")
+        b = torch.zeros_like(a)
+        p = dict(spp_sqrt=2, light_samples=2, use_bvh=True, seed=77)
+        ref = ds.render_tiles(ids, T, T, a.data_ptr(), rt.RenderParams(**p, sync=True))
+        assert ref.path == rt.PATH_STEPS and ref.rays > 0
+        st = ds.render_tiles(ids, T, T, b.data_ptr(), rt.RenderParams(**p, sync=False))
+        assert st.rays == ref.rays  # completed in the call
+        w = ds.wait()
+        assert w.rays == ref.rays and w.path == rt.PATH_STEPS and w.iterations == ref.iterations
+        assert ds.wait().rays == 0  # handed out once
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    finally:
+        ds.close()
         sc.close()

@@ -75,13 +75,14 @@ def _check(path, res, tiles, spp_sqrt, seed, slot_variants=()):
 
 def test_headline_soup_tiles_1024_100spp(soup_path, gpu):
     """bench.py's frame (1024^2, -s 10): the dense centre, the corners, an edge and two
-    off-centre tiles; then the same tiles with only 64K slots (every wave claims ~37
-    batches), and with one and three slot pipelines instead of two -- the scheduling must not
-    change a bit."""
+    off-centre tiles (one-pass); then the same tiles through the step pipeline with only 64K
+    slots (every wave claims ~37 batches), and with one and three slot pipelines -- the
+    scheduling must not change a bit."""
     tiles = [7 * 16 + 7, 8 * 16 + 8, 0, 15 * 16 + 15, 8 * 16 + 15, 3 * 16 + 12, 12 * 16 + 4]
     _check(soup_path, 1024, tiles, 10, seed=SOUP_SEED,
-           slot_variants=({"RT_SLOTS": "65536", "RT_LDS_STACK": "2"},
-                          {"RT_PIPES": "1"}, {"RT_PIPES": "3", "RT_LDS_STACK": "4"}))
+           slot_variants=({"RT_ONE_PASS": "0", "RT_SLOTS": "65536", "RT_LDS_STACK": "2"},
+                          {"RT_ONE_PASS": "0", "RT_PIPES": "1"},
+                          {"RT_ONE_PASS": "0", "RT_PIPES": "3", "RT_LDS_STACK": "4"}))
 
 
 def test_c5_tile_4096_64spp(soup_path, gpu):

@@ -8,7 +8,8 @@
 # Workloads: head (bench.py default, 10 steps), em2/em4/em8 (rank N-1's share of an N-way
 # split), c2 (primary only, 1 spp), c3 (Antialiasing), c4 (glossy + soft shadows), c5 (4096^2
 # x 64 spp).  Extra ENV=VAL arguments are exported for every run; BENCH_EXTRA="--flag ..." adds
-# bench.py arguments to every run.
+# bench.py arguments to every run.  Knob sweeps are ENV=VAL runs of one build, e.g.
+#   bash tools/ab.sh lib 1 "head em8 c5" RT_REFILL=40     (r04: refill / leaf thresholds)
 set -eo pipefail
 LIBS=${1:?builds}
 REPS=${2:-2}

@@ -1,11 +1,11 @@
 #!/bin/bash
 # One GPU measurement pass (run on the GPU box through gpurun):
-#   bash tools/measure_r04.sh LABEL [skip-tests]
+#   bash tools/measure.sh LABEL [skip-tests]
 # smoke + GPU parity tests; rocprofv3 kernel-trace stats of the headline bench; PMC passes
 # (FETCH_SIZE, WRITE_SIZE, the VALU set; one pass each, dispatches serialised by the profiler)
 # of the headline frame and of C5 (4096^2 x 64 spp), and the counter-measured VALU microbenchmark; the full headline bench (with the CPU
 # baseline) carrying the PMC summaries just measured; the other BASELINE configs (C2, C3,
-# C4, C5).  The per-rank shares of split frames: tools/measure_r04_shares.sh.  Everything lands
+# C4, C5).  The per-rank shares of split frames: tools/measure_shares.sh.  Everything lands
 # in gpurun_out/.
 set -eo pipefail
 L=${1:?label}

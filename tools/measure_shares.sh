@@ -1,6 +1,6 @@
 #!/bin/bash
 # Multi-GPU prediction from one GPU (run on the GPU box through gpurun):
-#   bash tools/measure_r04_shares.sh LABEL [DEAL] [SPLITS] [STEPS]
+#   bash tools/measure_shares.sh LABEL [DEAL] [SPLITS] [STEPS]
 # Every rank's share of the N-way splits (SPLITS, default "2 4 8") of the headline frame, and
 # of the 8-way split of C5 (4096^2 x 64 spp), each rendered alone on this GPU (bench.py
 # --emulate N --emulate-rank r --deal DEAL, default lattice); the whole frames for

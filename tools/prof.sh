@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel-trace profiles (rocprofv3 --kernel-trace --stats) of bench workloads on the current
-# build:  bash tools/r04_prof.sh LABEL "head em8 c3 ..."
+# build:  bash tools/prof.sh LABEL "head em8 c3 ..."
 source tools/gpu_steps.sh
 L=${1:?label}
 B=tests/golden/scenes/blend

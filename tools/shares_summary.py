@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""shares_summary.py -- slowest-rank prediction of the multi-GPU runs from tools/measure_r03_shares.sh.
+"""shares_summary.py -- slowest-rank prediction of the multi-GPU runs from tools/measure_shares.sh.
 
 For an N-way split every rank renders its lattice share alone on one GPU; with one GPU per
 rank the frame takes the slowest rank's time plus the gather.  Predicted N-GPU Mrays/s =
