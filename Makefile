@@ -38,11 +38,13 @@ $(BIN)/raytracer: $(SRC)/host/main.cpp $(LIB)/librt_host.so $(LIB)/librt_comm.so
 	@mkdir -p $(BIN)
 	$(CXX) $(CXXFLAGS) $(SRC)/host/main.cpp -o $@ -L$(LIB) -lrt_host -lrt_comm -lrt_hip -lpthread -Wl,-rpath,'$$ORIGIN/../lib'
 
-# A/B build of the HIP library with extra defines into ray_tracying_amd/lib_$(V)/ (diagnostic;
-# select it at run time with RT_LIB_DIR): make variant V=w5 VDEFS=-DRT_TRACE_WAVES=5
+# A/B build of the HIP library with extra defines (or another source, VSRC: e.g. the previous
+# commit's rt_hip.hip saved beside it) into ray_tracying_amd/lib_$(V)/ (diagnostic; select it
+# at run time with RT_LIB_DIR): make variant V=w5 VDEFS=-DRT_TRACE_WAVES=5
+VSRC ?= $(SRC)/hip/rt_hip.hip
 variant: $(LIB)/librt_host.so
 	@mkdir -p ray_tracying_amd/lib_$(V)
-	$(HIPCC) $(HIPFLAGS) $(VDEFS) -shared $(SRC)/hip/rt_hip.hip -o ray_tracying_amd/lib_$(V)/librt_hip.so
+	$(HIPCC) $(HIPFLAGS) $(VDEFS) -shared $(VSRC) -o ray_tracying_amd/lib_$(V)/librt_hip.so
 	cp $(LIB)/librt_host.so $(LIB)/librt_comm.so ray_tracying_amd/lib_$(V)/
 
 # Host code and oracle under AddressSanitizer + UndefinedBehaviorSanitizer (host only: the

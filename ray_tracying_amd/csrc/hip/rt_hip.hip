@@ -291,7 +291,6 @@ struct TraceArgs {
   // their tiles by
   unsigned int* tile_cost;
   FastDiv fd_tile_units;
-  float* help_hit;            // [n_threads][HIT_STRIDE]: a drain helper's closest-hit record
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
 #endif
@@ -347,14 +346,12 @@ __device__ __forceinline__ const float4* at_byte(const float4* base, uint32_t of
   return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + off);
 }
 
-// Tests primitives [first, first + cnt) against the lane's query.  Planes-only scenes without
-// textures store a new closest hit's record (Plane::intersect's hit point and the precomputed
-// normal, shapes.cpp:472-480, and the material) to the slot's hit record when it is found --
-// a closer hit overwrites it -- so the write-back needs no re-test and no register holds it
-// across the traversal.
-template <bool kCount, bool kPlanesOnly, bool kDrain = false>
-__device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int first, int cnt, const Ray& r, bool any,
-                                           float tmax, uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
+// Tests primitives [first, first + cnt) against the lane's query: only (t, reference index,
+// primitive index) of the best hit are kept; its hit record is written once, when the query
+// settles (finish_query).
+template <bool kCount, bool kPlanesOnly>
+__device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cnt, const Ray& r, bool any, float tmax,
+                                           uint32_t par, bool check_leaf, HitState& h, unsigned int& nprim) {
   for (int k = 0; k < cnt; ++k) {
     const int pi = first + k;
     const float4* rec = at_byte(a.c.prims, (uint32_t)pi * ((uint32_t)a.c.prim_stride4 << 4));  // pi < 2^24
@@ -365,9 +362,8 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
       ++nprim;
       if (a.diag && __lane_id() == __ffsll((long long)__ballot(1)) - 1) atomicAdd(a.counters + 61, 1ull);  // wave-level prim tests
     }
-    V3 X;
     if (kPlanesOnly) {
-      if (!plane_hit<false>(P, r, t, nullptr, &X)) continue;
+      if (!plane_hit<false>(P, r, t, nullptr)) continue;
     } else if (!prim_hit<false, false>(P, rec, r, t, nullptr)) {
       continue;
     }
@@ -387,11 +383,6 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int slot, int fir
       h.best_t = t;
       h.best_ref = ref.x;
       h.best_idx = pi;
-      if (kPlanesOnly && !a.has_tex) {  // a drain helper (no slot of its own): its lane's record
-        float* R = !kDrain || slot >= 0 ? hit_rec(a.hit, slot)
-                                        : a.help_hit + (size_t)(blockIdx.x * kBlock + threadIdx.x) * HIT_STRIDE;
-        store_hit_pnm(R, X, V3{P.a[3], P.a[7], P.a[11]}, RT_TAG_MATERIAL(prim_tag(P)));
-      }
     }
   }
 }
@@ -480,19 +471,30 @@ template <bool kCount, bool kPlanesOnly>
 __device__ __forceinline__ void complete_query(const TraceArgs& a, int slot, const Query& q, HitState& h,
                                                unsigned int& nprim) {
   if (a.c.use_bvh && !h.done && a.n_unbounded > 0)
-    test_prims<kCount, kPlanesOnly>(a, slot, a.c.n_prims - a.n_unbounded, a.n_unbounded, q.r, q.any, q.tmax, q.par, true, h,
-                                    nprim);
+    test_prims<kCount, kPlanesOnly>(a, a.c.n_prims - a.n_unbounded, a.n_unbounded, q.r, q.any, q.tmax, q.par, true, h, nprim);
 }
 
-// The result word and (closest hits) the hit record the logic step shades (planes-only scenes
-// without textures: already stored by test_prims when the hit was found).
+// The result word and (closest hits of planes-only scenes) the hit record the shading reads,
+// written once here: Plane::intersect's hit point o + t d from the best t (the same ops as the
+// test, so the same bits) and the record's precomputed normal (shapes.cpp:472-480) and
+// material -- in hp / hn too, for a fused shadow ray that follows (returns true then).
+// Transformed shapes get their record from the lane's settle (fused / soft-start instances) or
+// the logic step.
 template <bool kCount, bool kPlanesOnly>
-__device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const Query& q, HitState& h,
-                                             unsigned int& nprim) {
-  const int N = a.n_slots;
+__device__ __forceinline__ bool finish_query(const TraceArgs& a, int slot, const Query& q, HitState& h,
+                                             unsigned int& nprim, V3& hp, V3& hn) {
   const Ray& r = q.r;
   complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
   a.result[slot] = q.any ? (h.done ? 1 : 0) : h.best_idx;
+  if (kPlanesOnly && !a.has_tex && !q.any && h.best_idx >= 0) {
+    const float4* rec = at_byte(a.c.prims, (uint32_t)h.best_idx * ((uint32_t)a.c.prim_stride4 << 4));  // < 2^24
+    const float* w = reinterpret_cast<const float*>(rec);
+    hn = V3{w[3], w[7], w[11]};
+    const uint32_t tag = __float_as_uint(w[15]);
+    hp = V3{r.o.x + h.best_t * r.d.x, r.o.y + h.best_t * r.d.y, r.o.z + h.best_t * r.d.z};
+    store_hit_pnm(hit_rec(a.hit, slot), hp, hn, RT_TAG_MATERIAL(tag));
+    return true;
+  }
   if (kPlanesOnly && a.has_tex && !q.any && h.best_idx >= 0) {
     // textured planes: the hit record with (u, v) -- the same primitive test with attributes,
     // on the primitive this lane just tested (cached).  Scenes with transformed shapes get
@@ -507,7 +509,11 @@ __device__ __forceinline__ void finish_query(const TraceArgs& a, int slot, const
     prim_hit<true, true, true>(P, rec, r, t, &at);
     store_hit_pnm(hit_rec(a.hit, slot), at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
     a.hit_uv[slot] = make_float2(at.u, at.v);
+    hp = at.p;
+    hn = at.n;
+    return true;
   }
+  return false;
 }
 
 template <bool kCount>
@@ -743,7 +749,12 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 // leaf and node phases of trace_refill_kernel, and how often each runs, summed into the
 // control block (counters 64..71) and printed by rt_render_tiles.
 #ifdef RT_PHASE_TIMING
-#define RT_PT_DECL unsigned long long pt_c[4] = {0, 0, 0, 0}, pt_n[4] = {0, 0, 0, 0}, pt_t = __builtin_amdgcn_s_memtime();
+// (and the lanes doing useful work: pt_l[k] lane-iterations of useful work, pt_w[k] the
+// wave's capacity -- 64 per node phase; 64 x the longest leaf per leaf phase, whose useful
+// work is the primitive tests)
+#define RT_PT_DECL                                                                                   \
+  unsigned long long pt_c[4] = {0, 0, 0, 0}, pt_n[4] = {0, 0, 0, 0}, pt_l[4] = {0, 0, 0, 0},        \
+                     pt_w[4] = {0, 0, 0, 0}, pt_t = __builtin_amdgcn_s_memtime();
 #define RT_PT_MARK(k)                                           \
   do {                                                          \
     const unsigned long long pt_now = __builtin_amdgcn_s_memtime(); \
@@ -751,15 +762,23 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     pt_n[k] += 1;                                               \
     pt_t = pt_now;                                              \
   } while (0)
+#define RT_PT_LANES(k, useful, capacity) \
+  do {                                   \
+    pt_l[k] += (useful);                 \
+    pt_w[k] += (capacity);               \
+  } while (0)
 #define RT_PT_FLUSH                                               \
   if (lane == 0)                                                  \
     for (int k = 0; k < 4; ++k) {                                 \
       atomicAdd(ta.counters + 64 + k, pt_c[k]);                   \
       atomicAdd(ta.counters + 68 + k, pt_n[k]);                   \
+      atomicAdd(ta.counters + 72 + k, pt_l[k]);                   \
+      atomicAdd(ta.counters + 76 + k, pt_w[k]);                   \
     }
 #else
 #define RT_PT_DECL
 #define RT_PT_MARK(k)
+#define RT_PT_LANES(k, useful, capacity)
 #define RT_PT_FLUSH
 #endif
 #ifndef RT_TRACE_WAVES
@@ -822,19 +841,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     sw = stack_empty_word(sw);
     item = root_item;
     if (a.c.n_prims > 0 && !a.c.use_bvh)
-      test_prims<kCount, kPlanesOnly>(a, slot, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
+      test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
   };
   // kFuse: 0 while the lane traces the slot's own query; (occlusion bits << 8) | (light + 1)
   // while it traces the shadow ray of a point light for the closest hit it just found
   int fz = 0;
   // shade's shadow ray towards point light l from the slot's hit (raytracer.cpp:214-236; the
   // logic step's ops for it, on the hit record this kernel stored)
-  auto fused_shadow = [&](int l) {
-    const HitRec hr = load_hit(hit_rec(a.hit, slot));
+  // (the first light's: from the hit point / normal just computed; later lights reload them)
+  auto fused_shadow = [&](int l, V3 hp, V3 hn) {
     const rt_light& L = a.lights[l];
-    const V3 lv = sub(V3{L.location[0], L.location[1], L.location[2]}, hr.p);
+    const V3 lv = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
     const float tmax = sqrtf(dot(lv, lv));
-    setup_query(q, add(hr.p, mul(hr.n, 1e-4f)), normalize(lv), tmax, true);
+    setup_query(q, add(hp, mul(hn, 1e-4f)), normalize(lv), tmax, true);
     ++nrays;
     if (kCount) ++dg_any_rays;
     start_traversal();
@@ -872,11 +891,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   };
   // kSoft + soft_start: shade's first shadow ray for the closest hit just found (the logic
   // step's transition ST_CLOSEST -> ST_SHADOW, raytracer.cpp:180-236: light 0, sample 0)
-  auto soft_first = [&]() {
+  auto soft_first = [&](V3 hp, V3 hn) {
     const int N = a.n_slots;
     uint32_t* S = a.state;
     const uint32_t depth = S[F_CTRL * N + slot] >> 4;
-    const HitRec hr = load_hit(hit_rec(a.hit, slot));
     const rt_light& L = a.lights[0];
     V3 target{L.location[0], L.location[1], L.location[2]};
     if (L.radius > 0.0f) {
@@ -886,7 +904,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       target = add(target, mul(rng.in_unit_sphere(), L.radius));
       S[F_RNG * N + slot] = rng.ctr;
     }
-    const V3 lv = sub(target, hr.p);
+    const V3 lv = sub(target, hp);
     const float tmax = sqrtf(dot(lv, lv));
     S[F_CTRL * N + slot] = (uint32_t)ST_SHADOW | (depth << 4);
     S[F_LIGHT * N + slot] = 0u;
@@ -903,13 +921,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       S[(F_RAY + 1) * N + slot] = __float_as_uint(q.r.o.y);
       S[(F_RAY + 2) * N + slot] = __float_as_uint(q.r.o.z);
     }
-    setup_query(q, add(hr.p, mul(hr.n, 1e-4f)), normalize(lv), tmax, true);
+    setup_query(q, add(hp, mul(hn, 1e-4f)), normalize(lv), tmax, true);
     ++nrays;
     if (kCount) ++dg_any_rays;
     start_traversal();
   };
   auto settle = [&]() {
     int next = -1;  // kFuse: the light whose shadow ray the lane traces next
+    V3 hp{0.0f, 0.0f, 0.0f}, hn{0.0f, 0.0f, 0.0f};
+    bool have = false;  // hp / hn: the hit record just written (else the next shadow ray reloads it)
     if (kSoft && q.any) {
       complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
       if (soft_next(h.done)) return;
@@ -926,7 +946,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         fz = 0;
       }
     } else {
-      finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
+      have = finish_query<kCount, kPlanesOnly>(a, slot, q, h, nprim, hp, hn);
       if ((kFuse || (kSoft && a.soft_start)) && !q.any && h.best_idx >= 0) {
         if (!kPlanesOnly) {  // transformed shapes: the hit record the logic step would compute
           const float4* rec = a.c.prims + (size_t)h.best_idx * a.c.prim_stride4;
@@ -936,9 +956,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           float t;
           prim_hit<true, false, false>(P, rec, q.r, t, &at);
           store_hit_pnm(hit_rec(a.hit, slot), at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
+          hp = at.p;
+          hn = at.n;
+          have = true;
         }
         if (kSoft) {
-          soft_first();
+          soft_first(hp, hn);
           return;
         }
         if (a.n_fuse > 0) {  // (a one-pass call without lights launches this instance for the record alone)
@@ -947,8 +970,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         }
       }
     }
-    if (kFuse && next >= 0) fused_shadow(next);
-    else slot = -1;
+    if (kFuse && next >= 0) {
+      if (!have) {
+        const HitRec hr = load_hit(hit_rec(a.hit, slot));
+        hp = hr.p;
+        hn = hr.n;
+      }
+      fused_shadow(next, hp, hn);
+    } else {
+      slot = -1;
+    }
   };
   RT_PT_DECL
 #ifdef RT_EXIT_TIMING
@@ -1016,10 +1047,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
     const uint64_t leafm = __ballot(is_leaf_item(item));
     if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+#ifdef RT_PHASE_TIMING
+      {
+        const int c = is_leaf_item(item) ? (int)((uint32_t)item & 0x7fu) : 0;
+        int mx = c, sm = c;
+        for (int off = 32; off > 0; off >>= 1) {
+          mx = max(mx, __shfl_xor(mx, off));
+          sm += __shfl_xor(sm, off);
+        }
+        RT_PT_LANES(1, (unsigned long long)sm, 64ull * (unsigned long long)mx);
+      }
+#endif
       if (is_leaf_item(item)) {
         const uint32_t e = (uint32_t)item;
-        test_prims<kCount, kPlanesOnly>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
-                                        true, h, nprim);
+        test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par, true,
+                                        h, nprim);
         lim = cull_limit(a, q, h);
         item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
       }
@@ -1027,7 +1069,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     }
     // node phase
 #ifdef RT_PHASE_TIMING
-    if (__ballot(item >= 0) != 0ull) {
+    if (const uint64_t nm = __ballot(item >= 0)) {
+      RT_PT_LANES(2, (unsigned long long)__popcll(nm), 64ull);
       if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
       RT_PT_MARK(2);  // node phase
     }
@@ -1050,7 +1093,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     for (;;) {
       // fold finished helpers into their owners
       uint64_t fin = __ballot(own >= 0 && item == kNoItem);
-      if (fin != 0ull) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // helpers' records
       while (fin != 0ull) {
         const int hl = __ffsll((long long)fin) - 1;
         fin &= fin - 1ull;
@@ -1071,13 +1113,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
             h.best_ref = br;
             h.best_idx = bi;
             lim = cull_limit(a, q, h);
-            if (kPlanesOnly && !a.has_tex) {  // the helper's record becomes the slot's
-              const float4* src = reinterpret_cast<const float4*>(a.help_hit + (size_t)(gtid - lane + hl) * HIT_STRIDE);
-              float4* dst = reinterpret_cast<float4*>(hit_rec(a.hit, slot));
-              const float4 w0 = src[0], w1 = src[1];
-              dst[0] = w0;
-              dst[1] = w1;
-            }
           }
         }
       }
@@ -1148,8 +1183,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
         if (is_leaf_item(item)) {
           const uint32_t e = (uint32_t)item;
-          test_prims<kCount, kPlanesOnly, true>(a, slot, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax,
-                                                q.par, true, h, nprim);
+          test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
+                                          true, h, nprim);
           lim = cull_limit(a, q, h);
           item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
         }
@@ -2518,6 +2553,22 @@ static int print_exit_log(const TraceArgs& ta, float ms, int step) {
 }
 #endif
 
+#ifdef RT_PHASE_TIMING
+// diagnostic build: the traversal waves' time per phase (s_memtime ticks, executions) and the
+// lane utilisation of the node and leaf phases
+static int print_phase_timing(const unsigned long long* counters) {
+  unsigned long long pt[16] = {};
+  HIP_TRY(hipMemcpy(pt, counters + 64, sizeof(pt), hipMemcpyDeviceToHost), RT_EDEVICE);
+  const double tot = (double)(pt[0] + pt[1] + pt[2] + pt[3]);
+  std::fprintf(stderr, "[rt phase] refill %.3f (%llu), leaf %.3f (%llu), node %.3f (%llu), control %.3f (%llu) of %.3g wave-ticks; "
+               "lane utilisation: leaf %.3f (%.4g prim tests), node %.3f (%.4g visits)\n",
+               pt[0] / tot, pt[4], pt[1] / tot, pt[5], pt[2] / tot, pt[6], pt[3] / tot, pt[7], tot,
+               pt[13] ? (double)pt[9] / (double)pt[13] : 0.0, (double)pt[9], pt[14] ? (double)pt[10] / (double)pt[14] : 0.0,
+               (double)pt[10]);
+  return RT_OK;
+}
+#endif
+
 // Finishes the scene's enqueued one-pass call: waits for its last event, records its measured
 // tile costs (instrumented calls) and fills `stats` (may be null).
 static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
@@ -2542,13 +2593,7 @@ static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
   if (const int rc = print_exit_log(q.ta, ms, 0)) return rc;
 #endif
 #ifdef RT_PHASE_TIMING
-  {
-    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    HIP_TRY(hipMemcpy(pt, q.ta.counters + 64, sizeof(pt), hipMemcpyDeviceToHost), RT_EDEVICE);
-    const double tot = (double)(pt[0] + pt[1] + pt[2] + pt[3]);
-    std::fprintf(stderr, "[rt phase] refill %.3f (%llu), leaf %.3f (%llu), node %.3f (%llu), control %.3f (%llu) of %.3g wave-ticks\n",
-                 pt[0] / tot, pt[4], pt[1] / tot, pt[5], pt[2] / tot, pt[6], pt[3] / tot, pt[7], tot);
-  }
+  if (const int rc = print_phase_timing(q.ta.counters)) return rc;
 #endif
   s->last_iters = 1;
   if (!stats) return RT_OK;
@@ -2971,7 +3016,6 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   } pipes[kPipes];
   const int per_pipe = (n_slots / kBlock / n_pipes) * kBlock;
   const int spill_entries = std::max(0, s->desc.stack_bound - ta.lds_entries);
-  constexpr int kHelpHitEntries = HIT_STRIDE * 4 / 8;  // a helper's hit record, in spill entries (8 B)
   // a call of at most 4M units runs one short launch: one block per CU fewer shortens each
   // ray's latency and so the launch's tail (C2, 1M units: 6 / 5 / 4 blocks 1679 / 1772 / 1790
   // Mrays/s; one rank's eighth, 13M units: 5 and 6 within 1 %)
@@ -3003,7 +3047,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     P.logic_blocks = (unsigned)(count / kBlock);
     P.trace_blocks = std::min(grid_cap, (unsigned)((count + kBlock - 1) / kBlock));
     P.ta.n_threads = (int)P.trace_blocks * kBlock;
-    spill_need += (size_t)(spill_entries + kHelpHitEntries) * P.ta.n_threads;
+    spill_need += (size_t)spill_entries * P.ta.n_threads;
     P.iters = 0;
     P.steps = 0;
     P.done = false;
@@ -3018,8 +3062,6 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   for (int h = 0, off = 0; h < n_pipes; ++h) {  // each pipeline's traversal spills into its own range
     pipes[h].ta.spill = s->d_spill + (size_t)2 * off;
     off += spill_entries * pipes[h].ta.n_threads;
-    pipes[h].ta.help_hit = reinterpret_cast<float*>(s->d_spill + (size_t)2 * off);  // drain helpers' records after it
-    off += kHelpHitEntries * pipes[h].ta.n_threads;
   }
 #ifdef RT_EXIT_TIMING
   static unsigned long long* exit_log = nullptr;
@@ -3222,13 +3264,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     stats->iterations = iters;
     stats->path = one_pass ? RT_PATH_ONE_PASS : RT_PATH_STEPS;
 #ifdef RT_PHASE_TIMING
-    {
-      unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      HIP_TRY(hipMemcpy(pt, ctl + 4 + 2 * 64, sizeof(pt), hipMemcpyDeviceToHost), RT_EDEVICE);
-      const double tot = (double)(pt[0] + pt[1] + pt[2] + pt[3]);
-      std::fprintf(stderr, "[rt phase] refill %.3f (%llu), leaf %.3f (%llu), node %.3f (%llu), control %.3f (%llu) of %.3g wave-ticks\n",
-                   pt[0] / tot, pt[4], pt[1] / tot, pt[5], pt[2] / tot, pt[6], pt[3] / tot, pt[7], tot);
-    }
+    if (const int rc = print_phase_timing((unsigned long long*)(ctl + 4))) return rc;
 #endif
     stats->node_visits = 0;
     if (p->count_work) stats->node_visits = h_stats[61];  // lane-level node visits (trace_counters_out, ctl byte 488)
