@@ -648,10 +648,13 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
 // always miss; child entries come precomputed from the host (node index, or the encoded
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
+#ifndef RT_SPECULATE
+#define RT_SPECULATE 0  // A/B (make variant VDEFS=-DRT_SPECULATE=1): park the nearest leaf, go on with a node
+#endif
 template <bool kCount>
 __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, float lim, int node,
                                           const LaneStack& S, int& w, int gtid, unsigned int& nbox,
-                                          unsigned long long& dg_any_box, unsigned int& nvisit) {
+                                          unsigned long long& dg_any_box, unsigned int& nvisit, int& pleaf) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
   const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
@@ -718,6 +721,11 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   cswap_bits(t[0], c[0], t[2], c[2]);
   const bool v3 = __float_as_int(t[3]) != 0x7f800000, v2 = __float_as_int(t[2]) != 0x7f800000,
              v1 = __float_as_int(t[1]) != 0x7f800000;
+  // RT_SPECULATE: the nearest child is a leaf, another child was entered and no leaf is parked
+  // yet -- park it (tested with the wave's next leaf phase) and go on with child 1 instead of
+  // waiting: the lane does node work while it would otherwise idle (Aila & Laine's speculative
+  // traversal; any visiting order finds the same closest hit, ties to the lower reference index)
+  const bool park = RT_SPECULATE && v1 && pleaf == kNoItem && is_leaf_item(c[0]) && __float_as_int(t[0]) != 0x7f800000;
   // push the three other children (entries 3, 2, 1; far-to-near when fully sorted).  Writes
   // at sp, sp+v3, sp+v3+v2 -- offsets counting only the children entered -- leave exactly
   // those below the new top whatever the order (a missed one lands on the next slot and is
@@ -727,11 +735,15 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     *reinterpret_cast<int2*>(st) = make_int2(c[3], __float_as_int(t[3]));
     *reinterpret_cast<int2*>(st + (int)v3 * kStackRow) = make_int2(c[2], __float_as_int(t[2]));
     *reinterpret_cast<int2*>(st + ((int)v3 + (int)v2) * kStackRow) = make_int2(c[1], __float_as_int(t[1]));
-    w += ((int)v3 + (int)v2 + (int)v1) * kStackRow;
+    w += ((int)v3 + (int)v2 + (int)(v1 && !park)) * kStackRow;
   } else {
     if (v3) stack_push(a, S, w, gtid, c[3], t[3]);
     if (v2) stack_push(a, S, w, gtid, c[2], t[2]);
-    if (v1) stack_push(a, S, w, gtid, c[1], t[1]);
+    if (v1 && !park) stack_push(a, S, w, gtid, c[1], t[1]);
+  }
+  if (park) {
+    pleaf = c[0];
+    return c[1];
   }
   if (__float_as_int(t[0]) != 0x7f800000) return c[0];
   return stack_pop_live(a, S, w, gtid, lim);
@@ -825,6 +837,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   // lane state
   int slot = -1;        // query owned by this lane (traversing, or finished awaiting write-back)
   int item = kNoItem;   // node to visit / leaf to test next; kNoItem: traversal finished
+  int pleaf = kNoItem;  // RT_SPECULATE: a leaf parked for the next leaf phase while the lane visits nodes
   float lim = 0.0f;     // cull bound of the query (cull_limit), refreshed after each leaf test
   Query q;
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
@@ -840,6 +853,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     lim = cull_limit(a, q, h);
     sw = stack_empty_word(sw);
     item = root_item;
+    pleaf = kNoItem;
     if (a.c.n_prims > 0 && !a.c.use_bvh)
       test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
   };
@@ -988,9 +1002,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
 #endif
   for (;;) {
     RT_PT_MARK(3);  // loop control (ballots) since the node phase
-    uint64_t act = __ballot(item != kNoItem);
+    uint64_t act = __ballot(item != kNoItem || (RT_SPECULATE && pleaf != kNoItem));
     if (__popcll(act) < a.refill_min) {
-      if (slot >= 0 && item == kNoItem) settle();
+      if (slot >= 0 && item == kNoItem && (!RT_SPECULATE || pleaf == kNoItem)) settle();
       while (!exhausted) {
         const uint64_t freem = __ballot(slot < 0);
         if (freem == 0ull) break;
@@ -1037,16 +1051,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         }
         q_next += min(avail, (unsigned)__popcll(freem));
       }
-      act = __ballot(item != kNoItem);
+      act = __ballot(item != kNoItem || (RT_SPECULATE && pleaf != kNoItem));
       RT_PT_MARK(0);  // refill: write-back, work fetch, query setup
       // done when the queue is drained and every lane settled (a query with nothing to
       // traverse -- linear mode, empty scene -- is settled in the next refill phase)
       // (drain_help: the queries still traversing go on in the drain loop below)
       if (exhausted && (a.drain_help || __ballot(slot >= 0) == 0ull)) break;
     }
-    // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
-    const uint64_t leafm = __ballot(is_leaf_item(item));
-    if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+    // leaf phase: enough lanes wait on a leaf (RT_SPECULATE: or hold a parked one), or nothing
+    // else is left to do
+    const uint64_t leafm = __ballot(is_leaf_item(item) || (RT_SPECULATE && pleaf != kNoItem));
+    if (leafm != 0ull &&
+        (__popcll(leafm) >= a.leaf_min || (RT_SPECULATE ? __ballot(item >= 0) == 0ull : (act & ~leafm) == 0ull))) {
 #ifdef RT_PHASE_TIMING
       {
         const int c = is_leaf_item(item) ? (int)((uint32_t)item & 0x7fu) : 0;
@@ -1058,6 +1074,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         RT_PT_LANES(1, (unsigned long long)sm, 64ull * (unsigned long long)mx);
       }
 #endif
+#if RT_SPECULATE
+      if (pleaf != kNoItem || is_leaf_item(item)) {  // the parked leaf first; the item goes on
+        const bool parked = pleaf != kNoItem;
+        const uint32_t e = (uint32_t)(parked ? pleaf : item);
+        test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par, true,
+                                        h, nprim);
+        lim = cull_limit(a, q, h);
+        pleaf = kNoItem;
+        item = h.done ? kNoItem : parked ? item : stack_pop_live(a, S, sw, gtid, lim);
+      }
+#else
       if (is_leaf_item(item)) {
         const uint32_t e = (uint32_t)item;
         test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par, true,
@@ -1065,19 +1092,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         lim = cull_limit(a, q, h);
         item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
       }
+#endif
       RT_PT_MARK(1);  // leaf phase
     }
     // node phase
 #ifdef RT_PHASE_TIMING
     if (const uint64_t nm = __ballot(item >= 0)) {
       RT_PT_LANES(2, (unsigned long long)__popcll(nm), 64ull);
-      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
+      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit, pleaf);
       RT_PT_MARK(2);  // node phase
     }
 #else
-    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
+    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit, pleaf);
 #endif
   }
+#if RT_SPECULATE
+  // the drain loop parks nothing: a parked leaf becomes the lane's item again, the item it went
+  // on with goes back on the stack (t_near 0: never culled; the stack held it before)
+  if (pleaf != kNoItem) {
+    if (item != kNoItem) stack_push(a, S, sw, gtid, item, 0.0f);
+    item = pleaf;
+    pleaf = kNoItem;
+  }
+#endif
   // ---- drain (drain_help: the queue is dry).  A query still traversing keeps its lane (its
   // owner); a free lane becomes a helper: it takes the bottom entry of a busy lane's stack --
   // pushed first, the farthest subtree pending there -- and searches it with the owner's ray
@@ -1189,7 +1226,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
         }
       }
-      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
+      if (item >= 0) {
+        int no_park = 0;  // (a valid entry: never parks)
+        item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit, no_park);
+      }
     }
   }
   RT_PT_FLUSH
