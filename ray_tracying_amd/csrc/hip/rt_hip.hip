@@ -297,7 +297,6 @@ struct TraceArgs {
 };
 
 // ---------------------------------------------------------------- traversal
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 // The closest-hit / any-hit state of one query.
 struct HitState {
   float best_t;
@@ -648,13 +647,10 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
 // always miss; child entries come precomputed from the host (node index, or the encoded
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
-#ifndef RT_SPECULATE
-#define RT_SPECULATE 0  // A/B (make variant VDEFS=-DRT_SPECULATE=1): park the nearest leaf, go on with a node
-#endif
 template <bool kCount>
 __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, float lim, int node,
                                           const LaneStack& S, int& w, int gtid, unsigned int& nbox,
-                                          unsigned long long& dg_any_box, unsigned int& nvisit, int& pleaf) {
+                                          unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
   const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
@@ -671,18 +667,16 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   const uint32_t nxw = __builtin_amdgcn_perm(qa.y, qa.x, q.sel[0]), fxw = __builtin_amdgcn_perm(qa.x, qa.y, q.sel[0]);
   const uint32_t nyw = __builtin_amdgcn_perm(qa.w, qa.z, q.sel[1]), fyw = __builtin_amdgcn_perm(qa.z, qa.w, q.sel[1]);
   const uint32_t nzw = __builtin_amdgcn_perm(qb.y, qb.x, q.sel[2]), fzw = __builtin_amdgcn_perm(qb.x, qb.y, q.sel[2]);
-  const f32x2 Ax = {ax, ax}, Bx = {bx, bx}, Ay = {ay, ay}, By = {by, by}, Az = {az, az}, Bz = {bz, bz};
-  auto lo2 = [](uint32_t w) { return (f32x2){(float)(w & 0xffu), (float)((w >> 8) & 0xffu)}; };
-  auto hi2 = [](uint32_t w) { return (f32x2){(float)((w >> 16) & 0xffu), (float)(w >> 24)}; };
-  const f32x2 nx01 = __builtin_elementwise_fma(lo2(nxw), Bx, Ax), nx23 = __builtin_elementwise_fma(hi2(nxw), Bx, Ax);
-  const f32x2 fx01 = __builtin_elementwise_fma(lo2(fxw), Bx, Ax), fx23 = __builtin_elementwise_fma(hi2(fxw), Bx, Ax);
-  const f32x2 ny01 = __builtin_elementwise_fma(lo2(nyw), By, Ay), ny23 = __builtin_elementwise_fma(hi2(nyw), By, Ay);
-  const f32x2 fy01 = __builtin_elementwise_fma(lo2(fyw), By, Ay), fy23 = __builtin_elementwise_fma(hi2(fyw), By, Ay);
-  const f32x2 nz01 = __builtin_elementwise_fma(lo2(nzw), Bz, Az), nz23 = __builtin_elementwise_fma(hi2(nzw), Bz, Az);
-  const f32x2 fz01 = __builtin_elementwise_fma(lo2(fzw), Bz, Az), fz23 = __builtin_elementwise_fma(hi2(fzw), Bz, Az);
-  const float tnx[4] = {nx01.x, nx01.y, nx23.x, nx23.y}, tfx[4] = {fx01.x, fx01.y, fx23.x, fx23.y};
-  const float tny[4] = {ny01.x, ny01.y, ny23.x, ny23.y}, tfy[4] = {fy01.x, fy01.y, fy23.x, fy23.y};
-  const float tnz[4] = {nz01.x, nz01.y, nz23.x, nz23.y}, tfz[4] = {fz01.x, fz01.y, fz23.x, fz23.y};
+  // one v_fma_f32 per plane: on gfx950 it issues beside the byte converts, where a v_pk_fma_f32
+  // (two planes) does not (tools/ubench_mix.hip; r05 A/B: headline +2.5 %, one rank's eighth
+  // +2.6 %, C5 +3.6 %; the same fma per plane, so the same bits)
+  auto pl = [](uint32_t w, int k, float B, float A) { return __builtin_fmaf((float)((w >> (8 * k)) & 0xffu), B, A); };
+  const float tnx[4] = {pl(nxw, 0, bx, ax), pl(nxw, 1, bx, ax), pl(nxw, 2, bx, ax), pl(nxw, 3, bx, ax)};
+  const float tfx[4] = {pl(fxw, 0, bx, ax), pl(fxw, 1, bx, ax), pl(fxw, 2, bx, ax), pl(fxw, 3, bx, ax)};
+  const float tny[4] = {pl(nyw, 0, by, ay), pl(nyw, 1, by, ay), pl(nyw, 2, by, ay), pl(nyw, 3, by, ay)};
+  const float tfy[4] = {pl(fyw, 0, by, ay), pl(fyw, 1, by, ay), pl(fyw, 2, by, ay), pl(fyw, 3, by, ay)};
+  const float tnz[4] = {pl(nzw, 0, bz, az), pl(nzw, 1, bz, az), pl(nzw, 2, bz, az), pl(nzw, 3, bz, az)};
+  const float tfz[4] = {pl(fzw, 0, bz, az), pl(fzw, 1, bz, az), pl(fzw, 2, bz, az), pl(fzw, 3, bz, az)};
   if (kCount) {
     const uint32_t meta = qb.z;
     const uint64_t wm = __ballot(1);
@@ -721,11 +715,6 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   cswap_bits(t[0], c[0], t[2], c[2]);
   const bool v3 = __float_as_int(t[3]) != 0x7f800000, v2 = __float_as_int(t[2]) != 0x7f800000,
              v1 = __float_as_int(t[1]) != 0x7f800000;
-  // RT_SPECULATE: the nearest child is a leaf, another child was entered and no leaf is parked
-  // yet -- park it (tested with the wave's next leaf phase) and go on with child 1 instead of
-  // waiting: the lane does node work while it would otherwise idle (Aila & Laine's speculative
-  // traversal; any visiting order finds the same closest hit, ties to the lower reference index)
-  const bool park = RT_SPECULATE && v1 && pleaf == kNoItem && is_leaf_item(c[0]) && __float_as_int(t[0]) != 0x7f800000;
   // push the three other children (entries 3, 2, 1; far-to-near when fully sorted).  Writes
   // at sp, sp+v3, sp+v3+v2 -- offsets counting only the children entered -- leave exactly
   // those below the new top whatever the order (a missed one lands on the next slot and is
@@ -735,15 +724,11 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     *reinterpret_cast<int2*>(st) = make_int2(c[3], __float_as_int(t[3]));
     *reinterpret_cast<int2*>(st + (int)v3 * kStackRow) = make_int2(c[2], __float_as_int(t[2]));
     *reinterpret_cast<int2*>(st + ((int)v3 + (int)v2) * kStackRow) = make_int2(c[1], __float_as_int(t[1]));
-    w += ((int)v3 + (int)v2 + (int)(v1 && !park)) * kStackRow;
+    w += ((int)v3 + (int)v2 + (int)v1) * kStackRow;
   } else {
     if (v3) stack_push(a, S, w, gtid, c[3], t[3]);
     if (v2) stack_push(a, S, w, gtid, c[2], t[2]);
-    if (v1 && !park) stack_push(a, S, w, gtid, c[1], t[1]);
-  }
-  if (park) {
-    pleaf = c[0];
-    return c[1];
+    if (v1) stack_push(a, S, w, gtid, c[1], t[1]);
   }
   if (__float_as_int(t[0]) != 0x7f800000) return c[0];
   return stack_pop_live(a, S, w, gtid, lim);
@@ -837,7 +822,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   // lane state
   int slot = -1;        // query owned by this lane (traversing, or finished awaiting write-back)
   int item = kNoItem;   // node to visit / leaf to test next; kNoItem: traversal finished
-  int pleaf = kNoItem;  // RT_SPECULATE: a leaf parked for the next leaf phase while the lane visits nodes
   float lim = 0.0f;     // cull bound of the query (cull_limit), refreshed after each leaf test
   Query q;
   HitState h{__builtin_inff(), 0x7fffffff, -1, false};
@@ -853,7 +837,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     lim = cull_limit(a, q, h);
     sw = stack_empty_word(sw);
     item = root_item;
-    pleaf = kNoItem;
     if (a.c.n_prims > 0 && !a.c.use_bvh)
       test_prims<kCount, kPlanesOnly>(a, 0, a.c.n_prims, q.r, q.any, q.tmax, q.par, false, h, nprim);
   };
@@ -1002,9 +985,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
 #endif
   for (;;) {
     RT_PT_MARK(3);  // loop control (ballots) since the node phase
-    uint64_t act = __ballot(item != kNoItem || (RT_SPECULATE && pleaf != kNoItem));
+    uint64_t act = __ballot(item != kNoItem);
     if (__popcll(act) < a.refill_min) {
-      if (slot >= 0 && item == kNoItem && (!RT_SPECULATE || pleaf == kNoItem)) settle();
+      if (slot >= 0 && item == kNoItem) settle();
       while (!exhausted) {
         const uint64_t freem = __ballot(slot < 0);
         if (freem == 0ull) break;
@@ -1051,18 +1034,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         }
         q_next += min(avail, (unsigned)__popcll(freem));
       }
-      act = __ballot(item != kNoItem || (RT_SPECULATE && pleaf != kNoItem));
+      act = __ballot(item != kNoItem);
       RT_PT_MARK(0);  // refill: write-back, work fetch, query setup
       // done when the queue is drained and every lane settled (a query with nothing to
       // traverse -- linear mode, empty scene -- is settled in the next refill phase)
       // (drain_help: the queries still traversing go on in the drain loop below)
       if (exhausted && (a.drain_help || __ballot(slot >= 0) == 0ull)) break;
     }
-    // leaf phase: enough lanes wait on a leaf (RT_SPECULATE: or hold a parked one), or nothing
-    // else is left to do
-    const uint64_t leafm = __ballot(is_leaf_item(item) || (RT_SPECULATE && pleaf != kNoItem));
-    if (leafm != 0ull &&
-        (__popcll(leafm) >= a.leaf_min || (RT_SPECULATE ? __ballot(item >= 0) == 0ull : (act & ~leafm) == 0ull))) {
+    // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
+    const uint64_t leafm = __ballot(is_leaf_item(item));
+    if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
 #ifdef RT_PHASE_TIMING
       {
         const int c = is_leaf_item(item) ? (int)((uint32_t)item & 0x7fu) : 0;
@@ -1074,17 +1055,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         RT_PT_LANES(1, (unsigned long long)sm, 64ull * (unsigned long long)mx);
       }
 #endif
-#if RT_SPECULATE
-      if (pleaf != kNoItem || is_leaf_item(item)) {  // the parked leaf first; the item goes on
-        const bool parked = pleaf != kNoItem;
-        const uint32_t e = (uint32_t)(parked ? pleaf : item);
-        test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par, true,
-                                        h, nprim);
-        lim = cull_limit(a, q, h);
-        pleaf = kNoItem;
-        item = h.done ? kNoItem : parked ? item : stack_pop_live(a, S, sw, gtid, lim);
-      }
-#else
       if (is_leaf_item(item)) {
         const uint32_t e = (uint32_t)item;
         test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par, true,
@@ -1092,29 +1062,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         lim = cull_limit(a, q, h);
         item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
       }
-#endif
       RT_PT_MARK(1);  // leaf phase
     }
     // node phase
 #ifdef RT_PHASE_TIMING
     if (const uint64_t nm = __ballot(item >= 0)) {
       RT_PT_LANES(2, (unsigned long long)__popcll(nm), 64ull);
-      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit, pleaf);
+      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
       RT_PT_MARK(2);  // node phase
     }
 #else
-    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit, pleaf);
+    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
 #endif
   }
-#if RT_SPECULATE
-  // the drain loop parks nothing: a parked leaf becomes the lane's item again, the item it went
-  // on with goes back on the stack (t_near 0: never culled; the stack held it before)
-  if (pleaf != kNoItem) {
-    if (item != kNoItem) stack_push(a, S, sw, gtid, item, 0.0f);
-    item = pleaf;
-    pleaf = kNoItem;
-  }
-#endif
   // ---- drain (drain_help: the queue is dry).  A query still traversing keeps its lane (its
   // owner); a free lane becomes a helper: it takes the bottom entry of a busy lane's stack --
   // pushed first, the farthest subtree pending there -- and searches it with the owner's ray
@@ -1226,10 +1186,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
         }
       }
-      if (item >= 0) {
-        int no_park = 0;  // (a valid entry: never parks)
-        item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit, no_park);
-      }
+      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
     }
   }
   RT_PT_FLUSH

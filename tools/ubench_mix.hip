@@ -52,6 +52,55 @@ __global__ __launch_bounds__(256) void spin(float* out, float seed) {
       if (KIND == 20) { A1("v_fma_f32 %0, %0, %1, %2"); asm volatile("v_cmp_lt_u32 vcc, %0, %1" : : "v"(u[k]), "v"(v[k]) : "vcc"); }
       if (KIND == 21) A1("v_sub_f32 %0, %0, %1");
       if (KIND == 22) { A1("v_max3_f32 %0, %0, %1, %2"); asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(y[k]) : "v"(u[k])); }
+      // r05: the node visit's remaining kinds and the mixes a restructured visit would issue
+      if (KIND == 23) A1("v_max_f32 %0, %0, %1");
+      if (KIND == 24) U1("v_max_i32 %0, %0, %1");
+      if (KIND == 25) { A1("v_fma_f32 %0, %0, %1, %2"); U1("v_max_i32 %0, %0, %1"); }
+      if (KIND == 26) U1("v_cndmask_b32_e64 %0, %0, %1, s[20:21]");
+      if (KIND == 27) { A1("v_fma_f32 %0, %0, %1, %2"); U1("v_cndmask_b32_e64 %0, %0, %1, s[20:21]"); }
+      if (KIND == 28) A1("v_mul_f32 %0, %0, %1");
+      if (KIND == 29) U1("v_and_b32 %0, %0, %1");
+      if (KIND == 30) U1("v_lshlrev_b32 %0, %1, %0");
+      if (KIND == 31) {  // the node visit's planes as issued now: two byte converts per packed fma
+        asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(y[k]) : "v"(u[k]));
+        asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(z[k]) : "v"(u[k]));
+        asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(*(double*)&x[k & 6]) : "v"(*(double*)&y[k & 6]), "v"(*(double*)&z[k & 6]));
+      }
+      if (KIND == 32) {  // ... and with one scalar fma per converted byte
+        asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(y[k]) : "v"(u[k]));
+        A1("v_fma_f32 %0, %0, %1, %2");
+      }
+      if (KIND == 33) { A1("v_min_f32 %0, %0, %1"); U1("v_max_i32 %0, %0, %1"); }
+      if (KIND == 34) { A1("v_fma_f32 %0, %0, %1, %2"); A1("v_max_f32 %0, %0, %1"); }
+      if (KIND == 35) U1("v_med3_i32 %0, %0, %1, %2");
+      if (KIND == 36) { A1("v_fma_f32 %0, %0, %1, %2"); U1("v_max3_i32 %0, %0, %1, %2"); U1("v_perm_b32 %0, %0, %1, %2"); }
+      if (KIND == 37) U1("v_mul_u32_u24 %0, %0, %1");
+      if (KIND == 38) { A1("v_fma_f32 %0, %0, %1, %2"); U1("v_mul_u32_u24 %0, %0, %1"); }
+      if (KIND == 39) U1("v_or_b32 %0, %0, %1");
+      if (KIND == 40) U1("v_alignbit_b32 %0, %0, %1, %2");
+      if (KIND == 41) U1("v_bfe_u32 %0, %0, %1, %2");
+      if (KIND == 42) U1("v_lshrrev_b32 %0, %1, %0");
+      if (KIND == 43) A1("v_add_f32 %0, %0, %1");
+      if (KIND == 44) { A1("v_fma_f32 %0, %0, %1, %2"); U1("v_and_b32 %0, %0, %1"); }
+      if (KIND == 45) A1("v_ldexp_f32 %0, %0, %1");
+      if (KIND == 46) U1("v_xor_b32 %0, %0, %1");
+      if (KIND == 47) U1("v_sub_u32 %0, %0, %1");
+      if (KIND == 48) {  // bf16 plane pairs: one select, two extracts, two fmas per child-axis
+        U1("v_perm_b32 %0, %0, %1, %2");
+        asm volatile("v_and_b32 %0, 0xffff0000, %1" : "=v"(y[k]) : "v"(u[k]));
+        asm volatile("v_mul_u32_u24 %0, 0x10000, %1" : "=v"(z[k]) : "v"(u[k]));
+        A1("v_fma_f32 %0, %0, %1, %2");
+        A1("v_fma_f32 %0, %0, %2, %1");
+      }
+      if (KIND == 49) {  // byte planes as now (scalar): half a perm, two converts, two fmas per child-axis
+        if (k & 1) U1("v_perm_b32 %0, %0, %1, %2");
+        asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(y[k]) : "v"(u[k]));
+        asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(z[k]) : "v"(u[k]));
+        A1("v_fma_f32 %0, %0, %1, %2");
+        A1("v_fma_f32 %0, %0, %2, %1");
+      }
+      if (KIND == 50) { U1("v_sub_u32 %0, %0, %1"); U1("v_ashrrev_i32 %0, 31, %0"); U1("v_or_b32 %0, %0, %1"); }
+      if (KIND == 51) U1("v_ashrrev_i32 %0, 31, %0");
     }
   }
   float s = 0;
@@ -61,7 +110,7 @@ __global__ __launch_bounds__(256) void spin(float* out, float seed) {
 }
 
 template <int KIND>
-static void run(const char* name, int instr_per_k, int ncu) {
+static void run(const char* name, double instr_per_k, int ncu) {
   for (int wps : {1, 2, 4, 8}) {
     const int blocks = ncu * wps;  // 256-thread blocks: one wave per SIMD each
     float* out;
@@ -108,5 +157,34 @@ int main() {
   run<17>("pk_fma_f32 + max3_i32", 2, ncu);
   run<20>("fma_f32 + cmp_lt_u32", 2, ncu);
   run<22>("max3_f32 + cvt_f32_ubyte1", 2, ncu);
+  run<23>("v_max_f32", 1, ncu);
+  run<24>("v_max_i32", 1, ncu);
+  run<25>("fma_f32 + max_i32", 2, ncu);
+  run<26>("v_cndmask_b32_e64 (sgpr pair)", 1, ncu);
+  run<27>("fma_f32 + cndmask_e64", 2, ncu);
+  run<28>("v_mul_f32", 1, ncu);
+  run<29>("v_and_b32", 1, ncu);
+  run<30>("v_lshlrev_b32", 1, ncu);
+  run<31>("2 cvt_ubyte + pk_fma (planes now)", 3, ncu);
+  run<32>("cvt_ubyte + fma_f32 (scalar planes)", 2, ncu);
+  run<33>("min_f32 + max_i32", 2, ncu);
+  run<34>("fma_f32 + max_f32", 2, ncu);
+  run<35>("v_med3_i32", 1, ncu);
+  run<36>("fma_f32 + max3_i32 + perm", 3, ncu);
+  run<37>("v_mul_u32_u24", 1, ncu);
+  run<38>("fma_f32 + mul_u32_u24", 2, ncu);
+  run<39>("v_or_b32", 1, ncu);
+  run<40>("v_alignbit_b32", 1, ncu);
+  run<41>("v_bfe_u32", 1, ncu);
+  run<42>("v_lshrrev_b32", 1, ncu);
+  run<43>("v_add_f32", 1, ncu);
+  run<44>("fma_f32 + and_b32", 2, ncu);
+  run<45>("v_ldexp_f32", 1, ncu);
+  run<46>("v_xor_b32", 1, ncu);
+  run<47>("v_sub_u32", 1, ncu);
+  run<48>("bf16 pair: perm+and+mul_u24+2 fma", 5, ncu);
+  run<49>("bytes: 0.5 perm+2 cvt+2 fma", 4.5, ncu);
+  run<50>("sub_u32 + ashr + or (cull mask)", 3, ncu);
+  run<51>("v_ashrrev_i32", 1, ncu);
   return 0;
 }
