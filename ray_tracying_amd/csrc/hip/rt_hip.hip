@@ -405,6 +405,20 @@ __device__ __forceinline__ void cswap_bits(float& ta, int& ca, float& tb, int& c
   ca = c;
 }
 
+// cswap on unsigned keys (RT_CULL_MASK: t_near bits of an entered child, all ones for a miss)
+__device__ __forceinline__ void cswap_key(uint32_t& ka, int& ca, uint32_t& kb, int& cb) {
+  const bool sw = kb < ka;
+  const uint32_t lo = sw ? kb : ka, hi = sw ? ka : kb;
+  ka = lo;
+  kb = hi;
+  const int c = sw ? cb : ca;
+  cb = sw ? ca : cb;
+  ca = c;
+}
+#ifndef RT_CULL_MASK
+#define RT_CULL_MASK 0  // A/B: miss keys from an arithmetic shift instead of compare + select
+#endif
+
 // One query's traversal state between node steps.
 struct Query {
   Ray r;
@@ -647,12 +661,64 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
 // always miss; child entries come precomputed from the host (node index, or the encoded
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
+#ifndef RT_NODE_BF16
+#define RT_NODE_BF16 0  // A/B: 80-B device nodes with bf16 plane pairs (upload_nodes)
+#endif
 template <bool kCount>
 __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, float lim, int node,
                                           const LaneStack& S, int& w, int gtid, unsigned int& nbox,
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
+#if RT_NODE_BF16
+  // the device node (upload_nodes): origin + exponents, per axis the children's lo / hi codes as
+  // bf16 pairs (child 2k in the high half of a word, 2k + 1 in the low half), the child entries;
+  // `node` is its offset in 16-B units.  A bf16 code in a word's high half is its binary32 value
+  // with one v_and_b32, the low half with one v_mul_u32_u24 by 2^16 (both issue beside the fmas
+  // on gfx950; a byte convert or a shift does not): float(q) exactly, the byte layout's values.
+  const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 4);  // node / 5 < 2^26 (rt_scene_create)
+  const float4 g = nd[0];
+  const uint4 px = *reinterpret_cast<const uint4*>(nd + 1);
+  const uint4 py = *reinterpret_cast<const uint4*>(nd + 2);
+  const uint4 pz = *reinterpret_cast<const uint4*>(nd + 3);
+  const int4 qc = *reinterpret_cast<const int4*>(nd + 4);
+  const uint32_t ex = __float_as_uint(g.w);
+  const int cc[4] = {qc.x, qc.y, qc.z, qc.w};
+  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
+  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
+  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
+  // per axis and pair of children: perm(hi, lo, sel) is the near word, swapped the far one
+  auto hi16 = [](uint32_t w) { return __uint_as_float(w & 0xffff0000u); };
+  auto lo16 = [](uint32_t w) {
+    uint32_t r;
+    asm("v_mul_u32_u24 %0, 0x10000, %1" : "=v"(r) : "v"(w));
+    return __uint_as_float(r);
+  };
+  auto axis = [&](const uint4& p, uint32_t sel, float B, float A, float* tn, float* tf) {
+    const uint32_t n01 = __builtin_amdgcn_perm(p.y, p.x, sel), f01 = __builtin_amdgcn_perm(p.x, p.y, sel);
+    const uint32_t n23 = __builtin_amdgcn_perm(p.w, p.z, sel), f23 = __builtin_amdgcn_perm(p.z, p.w, sel);
+    tn[0] = __builtin_fmaf(hi16(n01), B, A);
+    tn[1] = __builtin_fmaf(lo16(n01), B, A);
+    tn[2] = __builtin_fmaf(hi16(n23), B, A);
+    tn[3] = __builtin_fmaf(lo16(n23), B, A);
+    tf[0] = __builtin_fmaf(hi16(f01), B, A);
+    tf[1] = __builtin_fmaf(lo16(f01), B, A);
+    tf[2] = __builtin_fmaf(hi16(f23), B, A);
+    tf[3] = __builtin_fmaf(lo16(f23), B, A);
+  };
+  float tnx[4], tfx[4], tny[4], tfy[4], tnz[4], tfz[4];
+  axis(px, q.sel[0], bx, ax, tnx, tfx);
+  axis(py, q.sel[1], by, ay, tny, tfy);
+  axis(pz, q.sel[2], bz, az, tnz, tfz);
+  if (kCount) {
+    const uint64_t wm = __ballot(1);
+    if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
+    ++nvisit;
+    const unsigned nb = (cc[0] != -1) + (cc[1] != -1) + (cc[2] != -1) + (cc[3] != -1);  // non-empty children
+    nbox += nb;
+    if (q.any) dg_any_box += nb;
+  }
+#else
   const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
   const float4 g = nd[0];
   const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
@@ -687,6 +753,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     nbox += nb;
     if (q.any) dg_any_box += nb;
   }
+#endif
   // entered within the bound: max(t_near, 0) <= min(t_far, lim)  (lim > 0 always), i.e.
   // t_near <= t_far, t_far >= 0 and t_near <= lim; misses sort last as (inf, entry)
   float t[4];
@@ -697,6 +764,37 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   // value no longer matters); a far distance of exactly -0 now fails too -- conservative, as
   // no accepted hit lies there (the origin would sit on a padded box's far face)
   const int lim_b = __float_as_int(lim);
+#if RT_CULL_MASK
+  // keys: an entered child's t_near bits (>= +0), a missed one all ones -- (fb - nb) >> 31 (a
+  // subtraction, an arithmetic shift and an or, which issue beside the compare / select class
+  // on gfx950) instead of a compare and a select; a wrap-around of fb - nb (fb a tiny negative,
+  // nb larger) only lets a box behind the ray in: conservative
+  uint32_t kk[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int nb = max(max(__float_as_int(tnx[k]), __float_as_int(tny[k])), max(__float_as_int(tnz[k]), 0));
+    const int fb = min(min(__float_as_int(tfx[k]), __float_as_int(tfy[k])), min(__float_as_int(tfz[k]), lim_b));
+    kk[k] = (uint32_t)nb | (uint32_t)((int)((uint32_t)fb - (uint32_t)nb) >> 31);
+    c[k] = cc[k];
+  }
+  cswap_key(kk[0], c[0], kk[1], c[1]);
+  cswap_key(kk[2], c[2], kk[3], c[3]);
+  cswap_key(kk[0], c[0], kk[2], c[2]);
+  const int v3 = (int)(~kk[3] >> 31), v2 = (int)(~kk[2] >> 31), v1 = (int)(~kk[1] >> 31);  // 1: entered
+  if (__ballot(w >= (a.lds_entries - 2) * kStackRow) == 0ull) {  // sp + 3 <= lds_entries in every lane
+    char* st = S.lds + w;
+    *reinterpret_cast<int2*>(st) = make_int2(c[3], (int)kk[3]);
+    *reinterpret_cast<int2*>(st + v3 * kStackRow) = make_int2(c[2], (int)kk[2]);
+    *reinterpret_cast<int2*>(st + (v3 + v2) * kStackRow) = make_int2(c[1], (int)kk[1]);
+    w += (v3 + v2 + v1) * kStackRow;
+  } else {
+    if (v3) stack_push(a, S, w, gtid, c[3], __uint_as_float(kk[3]));
+    if (v2) stack_push(a, S, w, gtid, c[2], __uint_as_float(kk[2]));
+    if (v1) stack_push(a, S, w, gtid, c[1], __uint_as_float(kk[1]));
+  }
+  if (kk[0] != 0xffffffffu) return c[0];
+  return stack_pop_live(a, S, w, gtid, lim);
+#else
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int nb = max(max(__float_as_int(tnx[k]), __float_as_int(tny[k])), max(__float_as_int(tnz[k]), 0));
@@ -732,6 +830,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   }
   if (__float_as_int(t[0]) != 0x7f800000) return c[0];
   return stack_pop_live(a, S, w, gtid, lim);
+#endif
 }
 
 // Refill kernel.  Lanes that finished their query are handed new slots (from the wave's
@@ -2346,9 +2445,42 @@ static int upload(void** dst, const void* src, size_t bytes) {
 
 // The 64-B nodes as laid out in HBM: AoS, one node = four consecutive 16-B words fetched by
 // one lane (an SoA layout -- word k of every node in array k -- measured 2.3 % slower, r04).
+#if RT_NODE_BF16
+// RT_NODE_BF16: transcoded to 80-B device nodes (node_visit): origin + exponents | per axis the
+// lo / hi codes of children (0, 1) and (2, 3) as bf16 pairs | the child entries, internal ones
+// as the child's offset in 16-B units (index * 5)
+static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
+  std::vector<uint32_t> t((size_t)n * 20);
+  auto bf = [](uint32_t q) {  // q < 256: its binary32 value has 16 zero low bits
+    const float f = (float)q;
+    uint32_t b;
+    std::memcpy(&b, &f, 4);
+    return b >> 16;
+  };
+  for (int32_t i = 0; i < n; ++i) {
+    const rt_node4& d = nodes[i];
+    uint32_t* o = &t[(size_t)i * 20];
+    std::memcpy(o, d.origin, 12);
+    o[3] = d.exps;
+    const uint32_t lo[3] = {d.q_lo_x, d.q_lo_y, d.q_lo_z}, hi[3] = {d.q_hi_x, d.q_hi_y, d.q_hi_z};
+    for (int ax = 0; ax < 3; ++ax)
+      for (int pr = 0; pr < 2; ++pr) {
+        auto code = [&](uint32_t w, int k) { return (w >> (8 * k)) & 0xffu; };
+        o[4 + 4 * ax + 2 * pr] = bf(code(lo[ax], 2 * pr)) << 16 | bf(code(lo[ax], 2 * pr + 1));
+        o[4 + 4 * ax + 2 * pr + 1] = bf(code(hi[ax], 2 * pr)) << 16 | bf(code(hi[ax], 2 * pr + 1));
+      }
+    for (int k = 0; k < 4; ++k) {
+      const bool internal = ((d.meta >> (8 * k)) & 0xffu) == 0x01u;
+      o[16 + k] = internal ? (uint32_t)(d.child[k] * 5) : (uint32_t)d.child[k];
+    }
+  }
+  return upload(dst, t.data(), t.size() * 4);
+}
+#else
 static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
   return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
 }
+#endif
 
 int rt_scene_destroy(rt_scene_t s) {
   if (!s) return RT_OK;
