@@ -765,16 +765,16 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   // no accepted hit lies there (the origin would sit on a padded box's far face)
   const int lim_b = __float_as_int(lim);
 #if RT_CULL_MASK
-  // keys: an entered child's t_near bits (>= +0), a missed one all ones -- (fb - nb) >> 31 (a
-  // subtraction, an arithmetic shift and an or, which issue beside the compare / select class
-  // on gfx950) instead of a compare and a select; a wrap-around of fb - nb (fb a tiny negative,
-  // nb larger) only lets a box behind the ray in: conservative
+  // keys: an entered child's t_near bits (>= +0), a missed one all ones -- fb >> 31 (a negative
+  // far distance) or (fb - nb) >> 31 (with fb, nb >= 0 no wrap-around) -- subtractions, arithmetic
+  // shifts and ors, which issue beside the compare / select class on gfx950, instead of a compare
+  // and a select
   uint32_t kk[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int nb = max(max(__float_as_int(tnx[k]), __float_as_int(tny[k])), max(__float_as_int(tnz[k]), 0));
     const int fb = min(min(__float_as_int(tfx[k]), __float_as_int(tfy[k])), min(__float_as_int(tfz[k]), lim_b));
-    kk[k] = (uint32_t)nb | (uint32_t)((int)((uint32_t)fb - (uint32_t)nb) >> 31);
+    kk[k] = (uint32_t)nb | (uint32_t)(fb >> 31) | (uint32_t)((int)((uint32_t)fb - (uint32_t)nb) >> 31);
     c[k] = cc[k];
   }
   cswap_key(kk[0], c[0], kk[1], c[1]);
