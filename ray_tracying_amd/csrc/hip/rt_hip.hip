@@ -282,6 +282,12 @@ struct TraceArgs {
   // frames / pinhole tell which of the closest ray's words the shading step reads back
   int soft_start;
   int frames, pinhole;
+  // kRefl launches (reflective scenes, one soft light, no refraction / textures): the light's last
+  // shadow sample of a reflective hit also shades it and traces its reflection ray in the lane
+  // (the logic step's Trace / shade ops on the slot's state, raytracer.cpp:180-331)
+  const rt_material* mats;
+  uint32_t* frames_buf;       // [kMaxDepth][FR_COUNT][n_slots]
+  float* query_rec;           // [Q_COUNT][n_slots]: the continued closest query, for the logic step
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
   int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
@@ -884,10 +890,15 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #ifndef RT_TRACE_WAVES_PLAIN
 #define RT_TRACE_WAVES_PLAIN 6  // every other instance: 6 waves/SIMD, 80 VGPRs (r03: plain headline
 #endif                          // +1.7 %, C5 +1.1 %; fused planes / soft shadows +1-2 %)
-// waves per SIMD of an instance: 5 only for fused shadows over transformed shapes (C3 -1..-3 % at 6)
-#define RT_INSTANCE_WAVES(kPlanesOnly, kFuse) ((kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : RT_TRACE_WAVES_PLAIN)
-template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse), 8))) void trace_refill_kernel(TraceArgs ta) {
+#ifndef RT_TRACE_WAVES_REFL
+#define RT_TRACE_WAVES_REFL 5  // reflection chains in the lane (kRefl): the shading code needs the registers
+#endif
+// waves per SIMD of an instance: 5 for fused shadows over transformed shapes (C3 -1..-3 % at 6)
+// and for reflection chains, else 6
+#define RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kRefl) \
+  (kRefl ? RT_TRACE_WAVES_REFL : (kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : RT_TRACE_WAVES_PLAIN)
+template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft, bool kRefl = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kRefl), 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_work;
   const int lane = threadIdx.x & 63;
@@ -1022,6 +1033,81 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     if (kCount) ++dg_any_rays;
     start_traversal();
   };
+  // kRefl: the last shadow sample of the scene's one (soft) light is done: if the hit reflects,
+  // finish shade (raytracer.cpp:180-274) and Trace's reflection step (:303-331) with the logic
+  // step's ops -- vis, the Blinn-Phong term, A = lc * final, the mirror / glossy ray from the
+  // slot's RNG stream -- write Trace's frame and the reflection query to the slot's state as the
+  // logic step would, and trace it in this lane; false (state untouched: the logic step redoes
+  // it, same draws) for a non-reflective hit, the depth limit or an invalid glossy ray
+  auto refl_next = [&](bool occluded) -> bool {
+    const int N = a.n_slots;
+    uint32_t* S = a.state;
+    const HitRec hr = load_hit(hit_rec(a.hit, slot));
+    const rt_material& m = a.mats[hr.mat];
+    const uint32_t ctrl = S[F_CTRL * N + slot];
+    const int depth = (int)(ctrl >> 4);
+    if (!(m.reflectivity > 0.0f) || depth + 1 > kMaxDepth) return false;
+    const uint32_t lw = S[F_LIGHT * N + slot];
+    const int ls = (int)(lw >> 16);
+    const rt_light& L = a.lights[0];
+    const int ns = (L.radius > 0.0f) ? a.light_samples : 1;
+    float vis = ls > 0 ? __uint_as_float(S[F_VIS * N + slot]) : 0.0f;
+    if (!occluded) vis += 1.0f;
+    const V3 ro{__uint_as_float(S[(F_RAY + 0) * N + slot]), __uint_as_float(S[(F_RAY + 1) * N + slot]),
+                __uint_as_float(S[(F_RAY + 2) * N + slot])};
+    const V3 rd{__uint_as_float(S[(F_RAY + 3) * N + slot]), __uint_as_float(S[(F_RAY + 4) * N + slot]),
+                __uint_as_float(S[(F_RAY + 5) * N + slot])};
+    const V3 hp = hr.p, hn = hr.n;
+    const V3 base{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
+    V3 fin{base.x * m.k_ambient, base.y * m.k_ambient, base.z * m.k_ambient};
+    vis = vis / (float)ns;
+    if (!(vis <= 0.0f)) {
+      const V3 V = normalize(sub(ro, hp));
+      const V3 lc = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
+      const float dsq = dot(lc, lc);
+      const float ldist = sqrtf(dsq);
+      const V3 Ld = normalize(lc);
+      const float ndl = smax(0.0f, dot(hn, Ld));
+      const V3 diff = mul(base, ndl);
+      const V3 H = normalize(add(Ld, V));
+      const float ndh = smax(0.0f, dot(hn, H));
+      const float si = rt_powf(ndh, m.shininess);
+      const V3 spec{m.specular[0] * si, m.specular[1] * si, m.specular[2] * si};
+      const float att = (10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq);
+      const V3 inner{diff.x * m.k_diffuse + spec.x * m.k_specular, diff.y * m.k_diffuse + spec.y * m.k_specular,
+                     diff.z * m.k_diffuse + spec.z * m.k_specular};
+      const V3 contrib{L.color[0] * inner.x * att, L.color[1] * inner.y * att, L.color[2] * inner.z * att};
+      fin = V3{fin.x + contrib.x * vis, fin.y + contrib.y * vis, fin.z + contrib.z * vis};
+    }
+    const float lcf = smax(0.0f, 1.0f - m.reflectivity - m.transparency);
+    const V3 A{lcf * fin.x, lcf * fin.y, lcf * fin.z};
+    // createReflectionRay (raytracer.cpp:101-115) + the glossy fuzz (:312-327)
+    const float idn = dot(rd, hn);
+    V3 rrd = sub(rd, mul(hn, 2.0f * idn));
+    const V3 rro = add(hp, mul(hn, 1e-4f));
+    Rng rng;
+    rng.key = (uint64_t)S[F_KEY * N + slot] | ((uint64_t)S[(F_KEY + 1) * N + slot] << 32);
+    rng.ctr = S[F_RNG * N + slot];
+    if (m.roughness > 0.0f) {
+      const V3 fuzz = rng.in_unit_sphere();
+      rrd = normalize(add(rrd, mul(fuzz, m.roughness)));
+      if (dot(rrd, hn) < 0.0f) rrd = V3{0.0f, 0.0f, 0.0f};
+    }
+    if (!(dot(rrd, rrd) > 0.001f)) return false;
+    // Trace's frame at this depth (reflection child pending) and the reflection query
+    uint32_t* F = a.frames_buf + (size_t)depth * FR_COUNT * N;
+    F[(FR_A + 0) * N + slot] = __float_as_uint(A.x);
+    F[(FR_A + 1) * N + slot] = __float_as_uint(A.y);
+    F[(FR_A + 2) * N + slot] = __float_as_uint(A.z);
+    F[FR_META * N + slot] = hr.mat << 2;
+    S[F_CTRL * N + slot] = (uint32_t)ST_CLOSEST | ((uint32_t)(depth + 1) << 4);
+    S[F_RNG * N + slot] = rng.ctr;
+    store_query(a.query_rec, N, slot, rro, rrd, 0.0f, 0);
+    setup_query(q, rro, rrd, 0.0f, false);  // secondary rays have time 0
+    ++nrays;
+    start_traversal();
+    return true;
+  };
   auto settle = [&]() {
     int next = -1;  // kFuse: the light whose shadow ray the lane traces next
     V3 hp{0.0f, 0.0f, 0.0f}, hn{0.0f, 0.0f, 0.0f};
@@ -1029,6 +1115,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     if (kSoft && q.any) {
       complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
       if (soft_next(h.done)) return;
+      if (kRefl && refl_next(h.done)) return;
       a.result[slot] = h.done ? 1 : 0;
     } else if (kFuse && fz != 0) {
       complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
@@ -2161,8 +2248,12 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
 }
 // trace launch (the refill kernel; count: the instrumented variant)
 template <bool kCount>
-void launch_trace2(const TraceArgs& ta, bool planes, bool soft, unsigned blocks, size_t lds, hipStream_t st) {
-  if (ta.n_fuse > 0 && planes)  // point lights only (the host's choice)
+void launch_trace2(const TraceArgs& ta, bool planes, bool soft, bool refl, unsigned blocks, size_t lds, hipStream_t st) {
+  if (soft && refl && planes)  // reflection chains continued in the lane (kRefl)
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else if (soft && refl)
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else if (ta.n_fuse > 0 && planes)  // point lights only (the host's choice)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (ta.n_fuse > 0 || (ta.one_pass && !planes))  // ... and no textures: the fused path stores no (u, v);
                                                        // one-pass calls of transformed shapes: the lane computes
@@ -2180,9 +2271,10 @@ void launch_trace2(const TraceArgs& ta, bool planes, bool soft, unsigned blocks,
     hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
 }
 // trace launch: soft = the lanes continue soft-light shadow samples themselves (kSoft)
-void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, unsigned blocks, size_t lds, hipStream_t st) {
-  if (count) launch_trace2<true>(ta, planes, soft, blocks, lds, st);
-  else launch_trace2<false>(ta, planes, soft, blocks, lds, st);
+void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, bool refl, unsigned blocks, size_t lds,
+                  hipStream_t st) {
+  if (count) launch_trace2<true>(ta, planes, soft, refl, blocks, lds, st);
+  else launch_trace2<false>(ta, planes, soft, refl, blocks, lds, st);
 }
 static int pipes_env() {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_PIPES");
@@ -2266,6 +2358,7 @@ struct rt_scene_s {
   void* d_ref_boxes = nullptr;
   int n_cu = 0, trace_blocks_per_cu = 0;  // plain traversal instance
   int trace_blocks_per_cu_fuse = 0, trace_blocks_per_cu_soft = 0;  // shadow-chain instances (kFuse / kSoft)
+  int trace_blocks_per_cu_refl = 0;  // kSoft with reflection chains (kRefl)
   bool late_draws = false;  // a light with radius > 0 or a rough material: draws after a sample's start
   bool soft_lights = false;  // a light with radius > 0 (several shadow samples with -light_sample > 1)
   int* d_spill = nullptr;
@@ -2618,6 +2711,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
                                                    : (const void*)trace_refill_kernel<false, false, true, false>, planes);
     s->trace_blocks_per_cu_soft = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, true>
                                                    : (const void*)trace_refill_kernel<false, false, false, true>, true);
+    s->trace_blocks_per_cu_refl = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, true, true>
+                                                   : (const void*)trace_refill_kernel<false, false, false, true, true>, true);
     s->n_cu = ncu;
     s->trace_blocks_per_cu = bpc;
   }
@@ -3072,6 +3167,16 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   if (const char* e = std::getenv("RT_SOFT_START")) ta.soft_start = ta.soft_start && std::atoi(e) != 0;
   ta.frames = need_frames ? 1 : 0;
   ta.pinhole = cam->aperture <= 0.0f ? 1 : 0;
+  // Reflection chains in the tracing lane (kRefl): the lane that traced a reflective hit's last
+  // soft-light sample shades the hit and traces its reflection ray (refl_next), so a sample's
+  // bounces take one step, not two each.  The lane shades light 0 only: scenes with one light,
+  // reflection without refraction, no textures.  RT_REFL_FUSE=0 leaves the chains to the logic step.
+  bool refl_trace = soft_trace && ta.soft_start && (s->desc.flags & RT_SCENE_HAS_REFLECTION) && !need_refr &&
+                    !(s->desc.flags & RT_SCENE_HAS_TEXTURE) && s->desc.n_lights == 1;
+  if (const char* e = std::getenv("RT_REFL_FUSE")) refl_trace = refl_trace && std::atoi(e) != 0;
+  ta.mats = (const rt_material*)s->d_mats;
+  ta.frames_buf = s->d_frames;
+  ta.query_rec = s->d_query;
   // Fused shadow rays halve the steps of a sample.  They pay when the call is small (at most
   // two slot loads of samples: one rank's share of a split frame; each launch ends in a drain
   // of ~0.45 ms whatever its size) and when the scene has few primitives (its frame is spent
@@ -3148,7 +3253,9 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // a call of at most 4M units runs one short launch: one block per CU fewer shortens each
   // ray's latency and so the launch's tail (C2, 1M units: 6 / 5 / 4 blocks 1679 / 1772 / 1790
   // Mrays/s; one rank's eighth, 13M units: 5 and 6 within 1 %)
-  const int call_bpc = fuse_launch ? s->trace_blocks_per_cu_fuse : soft_launch ? s->trace_blocks_per_cu_soft : s->trace_blocks_per_cu;
+  const int call_bpc = fuse_launch ? s->trace_blocks_per_cu_fuse
+                       : soft_launch ? (refl_trace ? s->trace_blocks_per_cu_refl : s->trace_blocks_per_cu_soft)
+                                     : s->trace_blocks_per_cu;
   // A deferred one-pass call (another frame in flight) leaves one block per CU to the other
   // frame's camera and shading kernels, which cannot share a CU's registers with six traversal
   // waves per SIMD (r04, one box, two frames in flight, Mrays/s: one rank's eighth / quarter
@@ -3255,7 +3362,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
-    launch_trace(P.ta, p->count_work != 0, planes_only, false, P.trace_blocks, lds, stream);
+    launch_trace(P.ta, p->count_work != 0, planes_only, false, false, P.trace_blocks, lds, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
     const unsigned rblocks = (unsigned)((n_pixels + kSrPixels - 1) / kSrPixels);
@@ -3313,7 +3420,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
-        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, P.trace_blocks, lds, P.st);
+        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, refl_trace, P.trace_blocks, lds, P.st);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
       }
