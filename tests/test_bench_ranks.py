@@ -33,6 +33,11 @@ def _bench(tmp_path, n, tag):
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == n
+    # the per-rank summary: every rank's wall / render / gather time and rays
+    rk = line["ranks"]
+    assert rk["n"] == n and len(rk["render_ms_per_step"]) == n and len(rk["gather_ms_per_step"]) == n
+    assert sum(rk["rays_per_step"]) == line["config"]["rays_per_step"]
+    assert 0 <= rk["slowest_rank"] < n and all(v > 0 for v in rk["render_ms_per_step"])
     return np.load(frame)
 
 
