@@ -47,12 +47,12 @@ namespace {
 constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
 constexpr int kBlock = 256;
 // default LDS stack entries per lane (RT_LDS_STACK overrides): 12 for the traversal instances
-// that run 6 waves/SIMD (6 blocks x 24 KB of LDS per CU), 16 for the one at 5 (fused
-// point-light shadows over transformed shapes: its hit-record code needs the registers)
-constexpr int kLdsStack = 16, kLdsStack6 = 12;
-static int lds_stack_entries(bool six_waves) {  // read per call: tests vary it within one process
+// that run 6 waves/SIMD (6 blocks x 24 KB of LDS per CU), 11 for the 7-wave ones (7 x 22 KB),
+// 16 for the one at 5 (fused point-light shadows over transformed shapes: its hit-record code
+// needs the registers)
+static int lds_stack_entries(int waves) {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_LDS_STACK");
-  return e ? std::max(1, std::min(64, std::atoi(e))) : six_waves ? kLdsStack6 : kLdsStack;
+  return e ? std::max(1, std::min(64, std::atoi(e))) : waves >= 7 ? 11 : waves == 6 ? 12 : 16;
 }
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
@@ -282,12 +282,6 @@ struct TraceArgs {
   // frames / pinhole tell which of the closest ray's words the shading step reads back
   int soft_start;
   int frames, pinhole;
-  // kRefl launches (reflective scenes, one soft light, no refraction / textures): the light's last
-  // shadow sample of a reflective hit also shades it and traces its reflection ray in the lane
-  // (the logic step's Trace / shade ops on the slot's state, raytracer.cpp:180-331)
-  const rt_material* mats;
-  uint32_t* frames_buf;       // [kMaxDepth][FR_COUNT][n_slots]
-  float* query_rec;           // [Q_COUNT][n_slots]: the continued closest query, for the logic step
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
   int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
@@ -410,20 +404,6 @@ __device__ __forceinline__ void cswap_bits(float& ta, int& ca, float& tb, int& c
   cb = sw ? ca : cb;
   ca = c;
 }
-
-// cswap on unsigned keys (RT_CULL_MASK: t_near bits of an entered child, all ones for a miss)
-__device__ __forceinline__ void cswap_key(uint32_t& ka, int& ca, uint32_t& kb, int& cb) {
-  const bool sw = kb < ka;
-  const uint32_t lo = sw ? kb : ka, hi = sw ? ka : kb;
-  ka = lo;
-  kb = hi;
-  const int c = sw ? cb : ca;
-  cb = sw ? ca : cb;
-  ca = c;
-}
-#ifndef RT_CULL_MASK
-#define RT_CULL_MASK 0  // A/B: miss keys from an arithmetic shift instead of compare + select
-#endif
 
 // One query's traversal state between node steps.
 struct Query {
@@ -667,64 +647,12 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
 // always miss; child entries come precomputed from the host (node index, or the encoded
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
-#ifndef RT_NODE_BF16
-#define RT_NODE_BF16 0  // A/B: 80-B device nodes with bf16 plane pairs (upload_nodes)
-#endif
 template <bool kCount>
 __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, float lim, int node,
                                           const LaneStack& S, int& w, int gtid, unsigned int& nbox,
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
-#if RT_NODE_BF16
-  // the device node (upload_nodes): origin + exponents, per axis the children's lo / hi codes as
-  // bf16 pairs (child 2k in the high half of a word, 2k + 1 in the low half), the child entries;
-  // `node` is its offset in 16-B units.  A bf16 code in a word's high half is its binary32 value
-  // with one v_and_b32, the low half with one v_mul_u32_u24 by 2^16 (both issue beside the fmas
-  // on gfx950; a byte convert or a shift does not): float(q) exactly, the byte layout's values.
-  const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 4);  // node / 5 < 2^26 (rt_scene_create)
-  const float4 g = nd[0];
-  const uint4 px = *reinterpret_cast<const uint4*>(nd + 1);
-  const uint4 py = *reinterpret_cast<const uint4*>(nd + 2);
-  const uint4 pz = *reinterpret_cast<const uint4*>(nd + 3);
-  const int4 qc = *reinterpret_cast<const int4*>(nd + 4);
-  const uint32_t ex = __float_as_uint(g.w);
-  const int cc[4] = {qc.x, qc.y, qc.z, qc.w};
-  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
-  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
-  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
-  // per axis and pair of children: perm(hi, lo, sel) is the near word, swapped the far one
-  auto hi16 = [](uint32_t w) { return __uint_as_float(w & 0xffff0000u); };
-  auto lo16 = [](uint32_t w) {
-    uint32_t r;
-    asm("v_mul_u32_u24 %0, 0x10000, %1" : "=v"(r) : "v"(w));
-    return __uint_as_float(r);
-  };
-  auto axis = [&](const uint4& p, uint32_t sel, float B, float A, float* tn, float* tf) {
-    const uint32_t n01 = __builtin_amdgcn_perm(p.y, p.x, sel), f01 = __builtin_amdgcn_perm(p.x, p.y, sel);
-    const uint32_t n23 = __builtin_amdgcn_perm(p.w, p.z, sel), f23 = __builtin_amdgcn_perm(p.z, p.w, sel);
-    tn[0] = __builtin_fmaf(hi16(n01), B, A);
-    tn[1] = __builtin_fmaf(lo16(n01), B, A);
-    tn[2] = __builtin_fmaf(hi16(n23), B, A);
-    tn[3] = __builtin_fmaf(lo16(n23), B, A);
-    tf[0] = __builtin_fmaf(hi16(f01), B, A);
-    tf[1] = __builtin_fmaf(lo16(f01), B, A);
-    tf[2] = __builtin_fmaf(hi16(f23), B, A);
-    tf[3] = __builtin_fmaf(lo16(f23), B, A);
-  };
-  float tnx[4], tfx[4], tny[4], tfy[4], tnz[4], tfz[4];
-  axis(px, q.sel[0], bx, ax, tnx, tfx);
-  axis(py, q.sel[1], by, ay, tny, tfy);
-  axis(pz, q.sel[2], bz, az, tnz, tfz);
-  if (kCount) {
-    const uint64_t wm = __ballot(1);
-    if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
-    ++nvisit;
-    const unsigned nb = (cc[0] != -1) + (cc[1] != -1) + (cc[2] != -1) + (cc[3] != -1);  // non-empty children
-    nbox += nb;
-    if (q.any) dg_any_box += nb;
-  }
-#else
   const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
   const float4 g = nd[0];
   const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
@@ -759,7 +687,6 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     nbox += nb;
     if (q.any) dg_any_box += nb;
   }
-#endif
   // entered within the bound: max(t_near, 0) <= min(t_far, lim)  (lim > 0 always), i.e.
   // t_near <= t_far, t_far >= 0 and t_near <= lim; misses sort last as (inf, entry)
   float t[4];
@@ -770,37 +697,6 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   // value no longer matters); a far distance of exactly -0 now fails too -- conservative, as
   // no accepted hit lies there (the origin would sit on a padded box's far face)
   const int lim_b = __float_as_int(lim);
-#if RT_CULL_MASK
-  // keys: an entered child's t_near bits (>= +0), a missed one all ones -- fb >> 31 (a negative
-  // far distance) or (fb - nb) >> 31 (with fb, nb >= 0 no wrap-around) -- subtractions, arithmetic
-  // shifts and ors, which issue beside the compare / select class on gfx950, instead of a compare
-  // and a select
-  uint32_t kk[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int nb = max(max(__float_as_int(tnx[k]), __float_as_int(tny[k])), max(__float_as_int(tnz[k]), 0));
-    const int fb = min(min(__float_as_int(tfx[k]), __float_as_int(tfy[k])), min(__float_as_int(tfz[k]), lim_b));
-    kk[k] = (uint32_t)nb | (uint32_t)(fb >> 31) | (uint32_t)((int)((uint32_t)fb - (uint32_t)nb) >> 31);
-    c[k] = cc[k];
-  }
-  cswap_key(kk[0], c[0], kk[1], c[1]);
-  cswap_key(kk[2], c[2], kk[3], c[3]);
-  cswap_key(kk[0], c[0], kk[2], c[2]);
-  const int v3 = (int)(~kk[3] >> 31), v2 = (int)(~kk[2] >> 31), v1 = (int)(~kk[1] >> 31);  // 1: entered
-  if (__ballot(w >= (a.lds_entries - 2) * kStackRow) == 0ull) {  // sp + 3 <= lds_entries in every lane
-    char* st = S.lds + w;
-    *reinterpret_cast<int2*>(st) = make_int2(c[3], (int)kk[3]);
-    *reinterpret_cast<int2*>(st + v3 * kStackRow) = make_int2(c[2], (int)kk[2]);
-    *reinterpret_cast<int2*>(st + (v3 + v2) * kStackRow) = make_int2(c[1], (int)kk[1]);
-    w += (v3 + v2 + v1) * kStackRow;
-  } else {
-    if (v3) stack_push(a, S, w, gtid, c[3], __uint_as_float(kk[3]));
-    if (v2) stack_push(a, S, w, gtid, c[2], __uint_as_float(kk[2]));
-    if (v1) stack_push(a, S, w, gtid, c[1], __uint_as_float(kk[1]));
-  }
-  if (kk[0] != 0xffffffffu) return c[0];
-  return stack_pop_live(a, S, w, gtid, lim);
-#else
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int nb = max(max(__float_as_int(tnx[k]), __float_as_int(tny[k])), max(__float_as_int(tnz[k]), 0));
@@ -836,7 +732,6 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   }
   if (__float_as_int(t[0]) != 0x7f800000) return c[0];
   return stack_pop_live(a, S, w, gtid, lim);
-#endif
 }
 
 // Refill kernel.  Lanes that finished their query are handed new slots (from the wave's
@@ -890,15 +785,12 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #ifndef RT_TRACE_WAVES_PLAIN
 #define RT_TRACE_WAVES_PLAIN 6  // every other instance: 6 waves/SIMD, 80 VGPRs (r03: plain headline
 #endif                          // +1.7 %, C5 +1.1 %; fused planes / soft shadows +1-2 %)
-#ifndef RT_TRACE_WAVES_REFL
-#define RT_TRACE_WAVES_REFL 5  // reflection chains in the lane (kRefl): the shading code needs the registers
-#endif
-// waves per SIMD of an instance: 5 for fused shadows over transformed shapes (C3 -1..-3 % at 6)
-// and for reflection chains, else 6
-#define RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kRefl) \
-  (kRefl ? RT_TRACE_WAVES_REFL : (kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : RT_TRACE_WAVES_PLAIN)
-template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft, bool kRefl = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kRefl), 8))) void trace_refill_kernel(TraceArgs ta) {
+// waves per SIMD of an instance: 5 only for fused shadows over transformed shapes (C3 -1..-3 % at
+// 6), 7 for the planes instances of whole frames (kSeven, chosen per call: render_tiles), else 6
+#define RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven) \
+  (kSeven ? 7 : (kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : RT_TRACE_WAVES_PLAIN)
+template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft, bool kSeven = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven), 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_work;
   const int lane = threadIdx.x & 63;
@@ -1033,81 +925,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     if (kCount) ++dg_any_rays;
     start_traversal();
   };
-  // kRefl: the last shadow sample of the scene's one (soft) light is done: if the hit reflects,
-  // finish shade (raytracer.cpp:180-274) and Trace's reflection step (:303-331) with the logic
-  // step's ops -- vis, the Blinn-Phong term, A = lc * final, the mirror / glossy ray from the
-  // slot's RNG stream -- write Trace's frame and the reflection query to the slot's state as the
-  // logic step would, and trace it in this lane; false (state untouched: the logic step redoes
-  // it, same draws) for a non-reflective hit, the depth limit or an invalid glossy ray
-  auto refl_next = [&](bool occluded) -> bool {
-    const int N = a.n_slots;
-    uint32_t* S = a.state;
-    const HitRec hr = load_hit(hit_rec(a.hit, slot));
-    const rt_material& m = a.mats[hr.mat];
-    const uint32_t ctrl = S[F_CTRL * N + slot];
-    const int depth = (int)(ctrl >> 4);
-    if (!(m.reflectivity > 0.0f) || depth + 1 > kMaxDepth) return false;
-    const uint32_t lw = S[F_LIGHT * N + slot];
-    const int ls = (int)(lw >> 16);
-    const rt_light& L = a.lights[0];
-    const int ns = (L.radius > 0.0f) ? a.light_samples : 1;
-    float vis = ls > 0 ? __uint_as_float(S[F_VIS * N + slot]) : 0.0f;
-    if (!occluded) vis += 1.0f;
-    const V3 ro{__uint_as_float(S[(F_RAY + 0) * N + slot]), __uint_as_float(S[(F_RAY + 1) * N + slot]),
-                __uint_as_float(S[(F_RAY + 2) * N + slot])};
-    const V3 rd{__uint_as_float(S[(F_RAY + 3) * N + slot]), __uint_as_float(S[(F_RAY + 4) * N + slot]),
-                __uint_as_float(S[(F_RAY + 5) * N + slot])};
-    const V3 hp = hr.p, hn = hr.n;
-    const V3 base{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
-    V3 fin{base.x * m.k_ambient, base.y * m.k_ambient, base.z * m.k_ambient};
-    vis = vis / (float)ns;
-    if (!(vis <= 0.0f)) {
-      const V3 V = normalize(sub(ro, hp));
-      const V3 lc = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
-      const float dsq = dot(lc, lc);
-      const float ldist = sqrtf(dsq);
-      const V3 Ld = normalize(lc);
-      const float ndl = smax(0.0f, dot(hn, Ld));
-      const V3 diff = mul(base, ndl);
-      const V3 H = normalize(add(Ld, V));
-      const float ndh = smax(0.0f, dot(hn, H));
-      const float si = rt_powf(ndh, m.shininess);
-      const V3 spec{m.specular[0] * si, m.specular[1] * si, m.specular[2] * si};
-      const float att = (10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq);
-      const V3 inner{diff.x * m.k_diffuse + spec.x * m.k_specular, diff.y * m.k_diffuse + spec.y * m.k_specular,
-                     diff.z * m.k_diffuse + spec.z * m.k_specular};
-      const V3 contrib{L.color[0] * inner.x * att, L.color[1] * inner.y * att, L.color[2] * inner.z * att};
-      fin = V3{fin.x + contrib.x * vis, fin.y + contrib.y * vis, fin.z + contrib.z * vis};
-    }
-    const float lcf = smax(0.0f, 1.0f - m.reflectivity - m.transparency);
-    const V3 A{lcf * fin.x, lcf * fin.y, lcf * fin.z};
-    // createReflectionRay (raytracer.cpp:101-115) + the glossy fuzz (:312-327)
-    const float idn = dot(rd, hn);
-    V3 rrd = sub(rd, mul(hn, 2.0f * idn));
-    const V3 rro = add(hp, mul(hn, 1e-4f));
-    Rng rng;
-    rng.key = (uint64_t)S[F_KEY * N + slot] | ((uint64_t)S[(F_KEY + 1) * N + slot] << 32);
-    rng.ctr = S[F_RNG * N + slot];
-    if (m.roughness > 0.0f) {
-      const V3 fuzz = rng.in_unit_sphere();
-      rrd = normalize(add(rrd, mul(fuzz, m.roughness)));
-      if (dot(rrd, hn) < 0.0f) rrd = V3{0.0f, 0.0f, 0.0f};
-    }
-    if (!(dot(rrd, rrd) > 0.001f)) return false;
-    // Trace's frame at this depth (reflection child pending) and the reflection query
-    uint32_t* F = a.frames_buf + (size_t)depth * FR_COUNT * N;
-    F[(FR_A + 0) * N + slot] = __float_as_uint(A.x);
-    F[(FR_A + 1) * N + slot] = __float_as_uint(A.y);
-    F[(FR_A + 2) * N + slot] = __float_as_uint(A.z);
-    F[FR_META * N + slot] = hr.mat << 2;
-    S[F_CTRL * N + slot] = (uint32_t)ST_CLOSEST | ((uint32_t)(depth + 1) << 4);
-    S[F_RNG * N + slot] = rng.ctr;
-    store_query(a.query_rec, N, slot, rro, rrd, 0.0f, 0);
-    setup_query(q, rro, rrd, 0.0f, false);  // secondary rays have time 0
-    ++nrays;
-    start_traversal();
-    return true;
-  };
   auto settle = [&]() {
     int next = -1;  // kFuse: the light whose shadow ray the lane traces next
     V3 hp{0.0f, 0.0f, 0.0f}, hn{0.0f, 0.0f, 0.0f};
@@ -1115,7 +932,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     if (kSoft && q.any) {
       complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
       if (soft_next(h.done)) return;
-      if (kRefl && refl_next(h.done)) return;
       a.result[slot] = h.done ? 1 : 0;
     } else if (kFuse && fz != 0) {
       complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
@@ -2248,11 +2064,11 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
 }
 // trace launch (the refill kernel; count: the instrumented variant)
 template <bool kCount>
-void launch_trace2(const TraceArgs& ta, bool planes, bool soft, bool refl, unsigned blocks, size_t lds, hipStream_t st) {
-  if (soft && refl && planes)  // reflection chains continued in the lane (kRefl)
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
-  else if (soft && refl)
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+void launch_trace2(const TraceArgs& ta, bool planes, bool soft, bool seven, unsigned blocks, size_t lds, hipStream_t st) {
+  if (!kCount && seven && planes && ta.n_fuse > 0)  // 7 waves/SIMD (whole frames; render_tiles)
+    hipLaunchKernelGGL((trace_refill_kernel<false, true, true, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+  else if (!kCount && seven && planes && !soft)
+    hipLaunchKernelGGL((trace_refill_kernel<false, true, false, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (ta.n_fuse > 0 && planes)  // point lights only (the host's choice)
     hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (ta.n_fuse > 0 || (ta.one_pass && !planes))  // ... and no textures: the fused path stores no (u, v);
@@ -2271,10 +2087,10 @@ void launch_trace2(const TraceArgs& ta, bool planes, bool soft, bool refl, unsig
     hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
 }
 // trace launch: soft = the lanes continue soft-light shadow samples themselves (kSoft)
-void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, bool refl, unsigned blocks, size_t lds,
+void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, bool seven, unsigned blocks, size_t lds,
                   hipStream_t st) {
-  if (count) launch_trace2<true>(ta, planes, soft, refl, blocks, lds, st);
-  else launch_trace2<false>(ta, planes, soft, refl, blocks, lds, st);
+  if (count) launch_trace2<true>(ta, planes, soft, seven, blocks, lds, st);
+  else launch_trace2<false>(ta, planes, soft, seven, blocks, lds, st);
 }
 static int pipes_env() {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_PIPES");
@@ -2358,7 +2174,7 @@ struct rt_scene_s {
   void* d_ref_boxes = nullptr;
   int n_cu = 0, trace_blocks_per_cu = 0;  // plain traversal instance
   int trace_blocks_per_cu_fuse = 0, trace_blocks_per_cu_soft = 0;  // shadow-chain instances (kFuse / kSoft)
-  int trace_blocks_per_cu_refl = 0;  // kSoft with reflection chains (kRefl)
+  int trace_blocks_per_cu_seven = 0, trace_blocks_per_cu_fuse_seven = 0;  // 7-wave planes instances
   bool late_draws = false;  // a light with radius > 0 or a rough material: draws after a sample's start
   bool soft_lights = false;  // a light with radius > 0 (several shadow samples with -light_sample > 1)
   int* d_spill = nullptr;
@@ -2538,42 +2354,9 @@ static int upload(void** dst, const void* src, size_t bytes) {
 
 // The 64-B nodes as laid out in HBM: AoS, one node = four consecutive 16-B words fetched by
 // one lane (an SoA layout -- word k of every node in array k -- measured 2.3 % slower, r04).
-#if RT_NODE_BF16
-// RT_NODE_BF16: transcoded to 80-B device nodes (node_visit): origin + exponents | per axis the
-// lo / hi codes of children (0, 1) and (2, 3) as bf16 pairs | the child entries, internal ones
-// as the child's offset in 16-B units (index * 5)
-static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
-  std::vector<uint32_t> t((size_t)n * 20);
-  auto bf = [](uint32_t q) {  // q < 256: its binary32 value has 16 zero low bits
-    const float f = (float)q;
-    uint32_t b;
-    std::memcpy(&b, &f, 4);
-    return b >> 16;
-  };
-  for (int32_t i = 0; i < n; ++i) {
-    const rt_node4& d = nodes[i];
-    uint32_t* o = &t[(size_t)i * 20];
-    std::memcpy(o, d.origin, 12);
-    o[3] = d.exps;
-    const uint32_t lo[3] = {d.q_lo_x, d.q_lo_y, d.q_lo_z}, hi[3] = {d.q_hi_x, d.q_hi_y, d.q_hi_z};
-    for (int ax = 0; ax < 3; ++ax)
-      for (int pr = 0; pr < 2; ++pr) {
-        auto code = [&](uint32_t w, int k) { return (w >> (8 * k)) & 0xffu; };
-        o[4 + 4 * ax + 2 * pr] = bf(code(lo[ax], 2 * pr)) << 16 | bf(code(lo[ax], 2 * pr + 1));
-        o[4 + 4 * ax + 2 * pr + 1] = bf(code(hi[ax], 2 * pr)) << 16 | bf(code(hi[ax], 2 * pr + 1));
-      }
-    for (int k = 0; k < 4; ++k) {
-      const bool internal = ((d.meta >> (8 * k)) & 0xffu) == 0x01u;
-      o[16 + k] = internal ? (uint32_t)(d.child[k] * 5) : (uint32_t)d.child[k];
-    }
-  }
-  return upload(dst, t.data(), t.size() * 4);
-}
-#else
 static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
   return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
 }
-#endif
 
 int rt_scene_destroy(rt_scene_t s) {
   if (!s) return RT_OK;
@@ -2697,8 +2480,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const bool planes = d->prim_stride == 64;
-    auto occupancy = [&](const void* fn, bool six_waves) {
-      const int lds_entries = std::min(d->stack_bound, lds_stack_entries(six_waves));
+    auto occupancy = [&](const void* fn, int waves) {
+      const int lds_entries = std::min(d->stack_bound, lds_stack_entries(waves));
       const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
       int b = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, lds_bytes) != hipSuccess || b < 1) b = 2;
@@ -2706,13 +2489,17 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
       return b;
     };
     bpc = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, false>
-                           : (const void*)trace_refill_kernel<false, false, false, false>, true);
+                           : (const void*)trace_refill_kernel<false, false, false, false>, 6);
     s->trace_blocks_per_cu_fuse = occupancy(planes ? (const void*)trace_refill_kernel<false, true, true, false>
-                                                   : (const void*)trace_refill_kernel<false, false, true, false>, planes);
+                                                   : (const void*)trace_refill_kernel<false, false, true, false>,
+                                            planes ? 6 : 5);
     s->trace_blocks_per_cu_soft = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, true>
-                                                   : (const void*)trace_refill_kernel<false, false, false, true>, true);
-    s->trace_blocks_per_cu_refl = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, true, true>
-                                                   : (const void*)trace_refill_kernel<false, false, false, true, true>, true);
+                                                   : (const void*)trace_refill_kernel<false, false, false, true>, 6);
+    if (planes) {
+      s->trace_blocks_per_cu_seven = occupancy((const void*)trace_refill_kernel<false, true, false, false, true>, 7);
+      s->trace_blocks_per_cu_fuse_seven = occupancy((const void*)trace_refill_kernel<false, true, true, false, true>, 7);
+    }
+
     s->n_cu = ncu;
     s->trace_blocks_per_cu = bpc;
   }
@@ -3146,7 +2933,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
-  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(true));  // set again below (instance)
+  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(6));  // set again below (instance)
   // the refill kernel's leaf items hold first << 7 in 31 bits
   ta.refill_min = refill_min_env();
   ta.leaf_min = leaf_min_env();
@@ -3167,16 +2954,6 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   if (const char* e = std::getenv("RT_SOFT_START")) ta.soft_start = ta.soft_start && std::atoi(e) != 0;
   ta.frames = need_frames ? 1 : 0;
   ta.pinhole = cam->aperture <= 0.0f ? 1 : 0;
-  // Reflection chains in the tracing lane (kRefl): the lane that traced a reflective hit's last
-  // soft-light sample shades the hit and traces its reflection ray (refl_next), so a sample's
-  // bounces take one step, not two each.  The lane shades light 0 only: scenes with one light,
-  // reflection without refraction, no textures.  RT_REFL_FUSE=0 leaves the chains to the logic step.
-  bool refl_trace = soft_trace && ta.soft_start && (s->desc.flags & RT_SCENE_HAS_REFLECTION) && !need_refr &&
-                    !(s->desc.flags & RT_SCENE_HAS_TEXTURE) && s->desc.n_lights == 1;
-  if (const char* e = std::getenv("RT_REFL_FUSE")) refl_trace = refl_trace && std::atoi(e) != 0;
-  ta.mats = (const rt_material*)s->d_mats;
-  ta.frames_buf = s->d_frames;
-  ta.query_rec = s->d_query;
   // Fused shadow rays halve the steps of a sample.  They pay when the call is small (at most
   // two slot loads of samples: one rank's share of a split frame; each launch ends in a drain
   // of ~0.45 ms whatever its size) and when the scene has few primitives (its frame is spent
@@ -3210,8 +2987,16 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   la.op_ft = op_ft;
   la.op_fk = op_fk;
   const bool fuse_launch = ta.n_fuse > 0 || (one_pass && !planes_only), soft_launch = !fuse_launch && soft_trace;
-  const bool six_waves = !(fuse_launch && !planes_only);
-  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(six_waves));
+  // Seven waves per SIMD (11 LDS stack entries) for the planes instances of synchronous calls of
+  // more than 32M units -- whole frames (r05, same box: headline +2.9 %, C5 +2.8 %, their 12 / 10
+  // spilled VGPRs outside the node visit); a deferred call (another frame in flight: one rank's
+  // eighth -2.6 %) and smaller calls keep six.  RT_TRACE_SEVEN=0 / 1 overrides (1: every planes
+  // call but soft-light and instrumented ones).
+  bool seven = planes_only && !soft_launch && !p->count_work && p->sync != 0 && n_units > (32LL << 20);
+  if (const char* e = std::getenv("RT_TRACE_SEVEN"))
+    seven = planes_only && !soft_launch && !p->count_work && std::atoi(e) != 0;
+  const int trace_waves = seven ? 7 : (fuse_launch && !planes_only) ? 5 : 6;
+  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(trace_waves));
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
   la.occl = s->d_occl;
@@ -3253,8 +3038,9 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // a call of at most 4M units runs one short launch: one block per CU fewer shortens each
   // ray's latency and so the launch's tail (C2, 1M units: 6 / 5 / 4 blocks 1679 / 1772 / 1790
   // Mrays/s; one rank's eighth, 13M units: 5 and 6 within 1 %)
-  const int call_bpc = fuse_launch ? s->trace_blocks_per_cu_fuse
-                       : soft_launch ? (refl_trace ? s->trace_blocks_per_cu_refl : s->trace_blocks_per_cu_soft)
+  const int call_bpc = seven ? (fuse_launch ? s->trace_blocks_per_cu_fuse_seven : s->trace_blocks_per_cu_seven)
+                       : fuse_launch ? s->trace_blocks_per_cu_fuse
+                       : soft_launch ? s->trace_blocks_per_cu_soft
                                      : s->trace_blocks_per_cu;
   // A deferred one-pass call (another frame in flight) leaves one block per CU to the other
   // frame's camera and shading kernels, which cannot share a CU's registers with six traversal
@@ -3362,7 +3148,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
-    launch_trace(P.ta, p->count_work != 0, planes_only, false, false, P.trace_blocks, lds, stream);
+    launch_trace(P.ta, p->count_work != 0, planes_only, false, seven, P.trace_blocks, lds, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
     const unsigned rblocks = (unsigned)((n_pixels + kSrPixels - 1) / kSrPixels);
@@ -3420,7 +3206,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
-        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, refl_trace, P.trace_blocks, lds, P.st);
+        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, seven, P.trace_blocks, lds, P.st);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
       }

@@ -61,6 +61,8 @@ KNOBS = [
     {"RT_DRAIN_HELP": "0"},  # no drain helpers: each query traversed by its own lane alone
     {"RT_DRAIN_HELP": "1", "RT_LDS_STACK": "2", "RT_LEAF_MIN": "1"},  # helpers take entries from the HBM spill area
     {"RT_DRAIN_HELP": "0", **STEPS},  # the step pipeline without helpers
+    {"RT_TRACE_SEVEN": "1"},  # the 7-wave planes instances (whole frames' default) on a small call
+    {"RT_TRACE_SEVEN": "1", "RT_LDS_STACK": "3", **STEPS},  # ... through the step pipeline, deep stacks spilling
     # step-pipeline knobs on a one-pass scene: ignored (one message each), still one-pass
     {"RT_FUSE": "1"},
     {"RT_FUSE": "0", "RT_SLOTS": "4096", "RT_PIPES": "2", "RT_DIAG": "1"},
