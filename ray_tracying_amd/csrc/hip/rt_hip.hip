@@ -787,8 +787,11 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #endif                          // +1.7 %, C5 +1.1 %; fused planes / soft shadows +1-2 %)
 // waves per SIMD of an instance: 5 only for fused shadows over transformed shapes (C3 -1..-3 % at
 // 6), 7 for the planes instances of whole frames (kSeven, chosen per call: render_tiles), else 6
+#ifndef RT_TRACE_WAVES_SOFT
+#define RT_TRACE_WAVES_SOFT RT_TRACE_WAVES_PLAIN  // soft-light chains over transformed shapes (A/B)
+#endif
 #define RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven) \
-  (kSeven ? 7 : (kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : RT_TRACE_WAVES_PLAIN)
+  (kSeven ? 7 : (kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : (kSoft && !kPlanesOnly) ? RT_TRACE_WAVES_SOFT : RT_TRACE_WAVES_PLAIN)
 template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft, bool kSeven = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven), 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
