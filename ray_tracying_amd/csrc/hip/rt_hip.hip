@@ -779,8 +779,8 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 #define RT_PT_FLUSH
 #endif
 #ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 5  // waves per SIMD the register allocation targets (A/B builds: make variant);
-                          // 5 fits without spills once the SLP vectoriser is off (Makefile)
+#define RT_TRACE_WAVES 6  // fused shadows over transformed shapes (C3; r05 A/B: 6 waves +4.2 % over 5
+                          // once the hit record moved to settle and the planes to scalar fmas)
 #endif
 #ifndef RT_TRACE_WAVES_PLAIN
 #define RT_TRACE_WAVES_PLAIN 6  // every other instance: 6 waves/SIMD, 80 VGPRs (r03: plain headline
@@ -788,10 +788,15 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 // waves per SIMD of an instance: 5 only for fused shadows over transformed shapes (C3 -1..-3 % at
 // 6), 7 for the planes instances of whole frames (kSeven, chosen per call: render_tiles), else 6
 #ifndef RT_TRACE_WAVES_SOFT
-#define RT_TRACE_WAVES_SOFT RT_TRACE_WAVES_PLAIN  // soft-light chains over transformed shapes (A/B)
+#define RT_TRACE_WAVES_SOFT 5  // soft-light chains over transformed shapes (C4; r05 A/B: +2.3 % over 6,
+                               // whose 30 spilled VGPRs sat in the chain code)
 #endif
 #define RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven) \
   (kSeven ? 7 : (kFuse && !kPlanesOnly) ? RT_TRACE_WAVES : (kSoft && !kPlanesOnly) ? RT_TRACE_WAVES_SOFT : RT_TRACE_WAVES_PLAIN)
+// the same choice on the host (LDS stack entries and blocks per CU of a launch)
+static int instance_waves(bool planes, bool fuse, bool soft, bool seven) {
+  return seven ? 7 : (fuse && !planes) ? RT_TRACE_WAVES : (soft && !planes) ? RT_TRACE_WAVES_SOFT : RT_TRACE_WAVES_PLAIN;
+}
 template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft, bool kSeven = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven), 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
@@ -2492,12 +2497,14 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
       return b;
     };
     bpc = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, false>
-                           : (const void*)trace_refill_kernel<false, false, false, false>, 6);
+                           : (const void*)trace_refill_kernel<false, false, false, false>,
+                    instance_waves(planes, false, false, false));
     s->trace_blocks_per_cu_fuse = occupancy(planes ? (const void*)trace_refill_kernel<false, true, true, false>
                                                    : (const void*)trace_refill_kernel<false, false, true, false>,
-                                            planes ? 6 : 5);
+                                            instance_waves(planes, true, false, false));
     s->trace_blocks_per_cu_soft = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, true>
-                                                   : (const void*)trace_refill_kernel<false, false, false, true>, 6);
+                                                   : (const void*)trace_refill_kernel<false, false, false, true>,
+                                            instance_waves(planes, false, true, false));
     if (planes) {
       s->trace_blocks_per_cu_seven = occupancy((const void*)trace_refill_kernel<false, true, false, false, true>, 7);
       s->trace_blocks_per_cu_fuse_seven = occupancy((const void*)trace_refill_kernel<false, true, true, false, true>, 7);
@@ -2998,7 +3005,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   bool seven = planes_only && !soft_launch && !p->count_work && p->sync != 0 && n_units > (32LL << 20);
   if (const char* e = std::getenv("RT_TRACE_SEVEN"))
     seven = planes_only && !soft_launch && !p->count_work && std::atoi(e) != 0;
-  const int trace_waves = seven ? 7 : (fuse_launch && !planes_only) ? 5 : 6;
+  const int trace_waves = instance_waves(planes_only, fuse_launch, soft_launch, seven);
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(trace_waves));
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
