@@ -242,6 +242,9 @@ struct LogicArgs {
   int op_fo, op_ft, op_fk;
 };
 
+#ifndef RT_CAM_IN_TRACE
+#define RT_CAM_IN_TRACE 0
+#endif
 struct TraceArgs {
   Common c;
   const int2* prim_refs;      // (reference index, reference leaf) per primitive
@@ -291,6 +294,13 @@ struct TraceArgs {
   // their tiles by
   unsigned int* tile_cost;
   FastDiv fd_tile_units;
+#if RT_CAM_IN_TRACE
+  // A/B variant: pinhole one-pass calls generate each unit's camera ray
+  // at refill (sample_ray on this copy of the call's LogicArgs) instead of reading camera_kernel's
+  // query record (skipping that kernel and its 12 B per unit of writes and reads)
+  LogicArgs cam_gen_args;
+  int cam_gen;
+#endif
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
 #endif
@@ -440,8 +450,108 @@ __device__ __forceinline__ void setup_query(Query& q, V3 o, V3 d, float tq, bool
   q.sel[2] = q.inv.z < 0.0f ? 0x07060504u : 0x03020100u;
 }
 
+// Camera::pixelToRay_thin_lens (camera.cpp:98-179), basis precomputed on the host.
+// The divisions px / res and those of the normalisations are correctly rounded quotients by
+// a precomputed reciprocal (rt_div.h: the same bits, a third of the instructions).
+__device__ __forceinline__ Ray camera_ray(const rt_camera_desc& c, float px, float py, Rng& rng, float inv_rx,
+                                          float inv_ry) {
+  float nx = 1.0f - rt_div_by(px, (float)c.res_x, inv_rx) * 2.0f;
+  float ny = 1.0f - rt_div_by(py, (float)c.res_y, inv_ry) * 2.0f;
+  float nxr = nx * c.half_sensor_w, nyr = ny * c.half_sensor_h;
+  V3 dw{c.x_dir[0] * nxr + c.y_dir[0] * nyr + c.z_dir[0] * c.focal_length,
+        c.x_dir[1] * nxr + c.y_dir[1] * nyr + c.z_dir[1] * c.focal_length,
+        c.x_dir[2] * nxr + c.y_dir[2] * nyr + c.z_dir[2] * c.focal_length};
+  dw = normalize_rcp(dw);
+  Ray r;
+  r.time = 0.0f;
+  V3 loc{c.location[0], c.location[1], c.location[2]};
+  if (c.aperture <= 0.0f) {
+    r.o = loc;
+    r.d = dw;
+    return r;
+  }
+  V3 fp{loc.x + dw.x * c.focus_dist, loc.y + dw.y * c.focus_dist, loc.z + dw.z * c.focus_dist};
+  float rx, ry;
+  for (;;) {  // random_in_unit_disk (camera.cpp:90-96)
+    rx = (float)rng.next() * 2.0f - 1.0f;
+    ry = (float)rng.next() * 2.0f - 1.0f;
+    if (rx * rx + ry * ry < 1.0f) break;
+  }
+  float lr = c.aperture / 2.0f;
+  rx *= lr;
+  ry *= lr;
+  V3 off{c.x_dir[0] * rx + c.y_dir[0] * ry, c.x_dir[1] * rx + c.y_dir[1] * ry,
+         c.x_dir[2] * rx + c.y_dir[2] * ry};
+  r.o = add(loc, off);
+  r.d = normalize_rcp(sub(fp, r.o));
+  return r;
+}
+
+// launch-local pixel index -> image (x, y) and output offset; 8x8 blocks inside tiles so
+// consecutive slots trace spatially coherent rays.
+__device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, int& y, size_t& out_off) {
+  const int tile_px = a.tile_w * a.tile_h;
+  const int tl = (int)fdiv((uint32_t)p, a.fd_tile_px), r = p - tl * tile_px;
+  const int b = r >> 6, l = r & 63;
+  const int by = (int)fdiv((uint32_t)b, a.fd_sub_x), bx = b - by * a.sub_x;
+  const int lx = bx * 8 + (l & 7), ly = by * 8 + (l >> 3);
+  const int tid = a.tile_affine ? a.tile_first + tl * a.tile_step : a.tile_ids[tl];
+  const int ty = (int)fdiv((uint32_t)tid, a.fd_tiles_x), tx = tid - ty * a.tiles_x;
+  x = tx * a.tile_w + lx;
+  y = ty * a.tile_h + ly;
+  const int to = a.tile_out ? a.tile_out[tl] : tl;
+  out_off = ((size_t)to * tile_px + (size_t)ly * a.tile_w + lx) * 3;
+  return x < a.cam.res_x && y < a.cam.res_y;
+}
+
+// ---------------------------------------------------------------- logic kernel
+// unit -> (launch-local pixel, sample); false if the pixel lies outside the image
+__device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, int& px, int& py, int& sample) {
+  // units < 2^31 (checked on the host): 32-bit unsigned division
+  const unsigned u = (unsigned)unit, ns = (unsigned)a.n_samples;
+  const int p = (int)fdiv(u, a.fd_samples);
+  sample = (int)(u - (unsigned)p * ns);
+  size_t off;
+  return pixel_coords(a, p, px, py, off);
+}
+
+// compute_pixel_color (raytracer.cpp:18-70): the camera ray of sample `sample` of pixel (px,
+// py) -- its RNG stream, the stratified jitter in double, Camera::pixelToRay_thin_lens (the
+// lens draws for an aperture > 0).  The ray's time is the caller's next draw.
+__device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, int sample, Rng& rng) {
+  rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
+  const int s = a.spp_sqrt;
+  float fx, fy;
+  if (s <= 1) {
+    fx = (float)px + 0.5f;
+    fy = (float)py + 0.5f;
+  } else {  // the divisions by s: fast invariant integer division, Markstein quotients (rt_div.h)
+    const int sj = (int)fdiv((uint32_t)sample, a.fd_s), si = sample - sj * s;
+    double ox = rng.next();
+    double oy = rng.next();
+    double sx = rt_div_by((double)si + ox, (double)s, a.inv_s);
+    double sy = rt_div_by((double)sj + oy, (double)s, a.inv_s);
+    fx = (float)((double)px + sx);
+    fy = (float)((double)py + sy);
+  }
+  return camera_ray(a.cam, fx, fy, rng, a.inv_res_x, a.inv_res_y);
+}
+
 // Reads slot's query record; false if the slot emitted no query this step.
 __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query& q) {
+#if RT_CAM_IN_TRACE
+  if (a.cam_gen) {  // the unit's camera ray, generated here (camera_kernel's ops)
+    int px, py, sample;
+    if (!unit_coords(a.cam_gen_args, (long long)(unsigned)slot, px, py, sample)) {
+      a.result[slot] = -1;
+      return false;
+    }
+    Rng rng;
+    const Ray ray = sample_ray(a.cam_gen_args, px, py, sample, rng);
+    setup_query(q, ray.o, ray.d, a.op_ft >= 0 ? (float)rng.next() : 0.0f, false);
+    return true;
+  }
+#endif
   if (a.one_pass) {  // the unit's camera ray (camera_kernel): 64-bit field offsets (up to 2^30 slots)
     const size_t n = (size_t)(unsigned)a.n_slots, u = (size_t)(unsigned)slot;
     if (a.op_fk >= 0 && __float_as_int(a.query[(size_t)a.op_fk * n + u]) < 0) return false;
@@ -1229,71 +1339,6 @@ __device__ __forceinline__ V3 diffuse_color(const LogicArgs& a, const rt_materia
   return V3{t.x * dc.x, t.y * dc.y, t.z * dc.z};
 }
 
-// Camera::pixelToRay_thin_lens (camera.cpp:98-179), basis precomputed on the host.
-// The divisions px / res and those of the normalisations are correctly rounded quotients by
-// a precomputed reciprocal (rt_div.h: the same bits, a third of the instructions).
-__device__ __forceinline__ Ray camera_ray(const rt_camera_desc& c, float px, float py, Rng& rng, float inv_rx,
-                                          float inv_ry) {
-  float nx = 1.0f - rt_div_by(px, (float)c.res_x, inv_rx) * 2.0f;
-  float ny = 1.0f - rt_div_by(py, (float)c.res_y, inv_ry) * 2.0f;
-  float nxr = nx * c.half_sensor_w, nyr = ny * c.half_sensor_h;
-  V3 dw{c.x_dir[0] * nxr + c.y_dir[0] * nyr + c.z_dir[0] * c.focal_length,
-        c.x_dir[1] * nxr + c.y_dir[1] * nyr + c.z_dir[1] * c.focal_length,
-        c.x_dir[2] * nxr + c.y_dir[2] * nyr + c.z_dir[2] * c.focal_length};
-  dw = normalize_rcp(dw);
-  Ray r;
-  r.time = 0.0f;
-  V3 loc{c.location[0], c.location[1], c.location[2]};
-  if (c.aperture <= 0.0f) {
-    r.o = loc;
-    r.d = dw;
-    return r;
-  }
-  V3 fp{loc.x + dw.x * c.focus_dist, loc.y + dw.y * c.focus_dist, loc.z + dw.z * c.focus_dist};
-  float rx, ry;
-  for (;;) {  // random_in_unit_disk (camera.cpp:90-96)
-    rx = (float)rng.next() * 2.0f - 1.0f;
-    ry = (float)rng.next() * 2.0f - 1.0f;
-    if (rx * rx + ry * ry < 1.0f) break;
-  }
-  float lr = c.aperture / 2.0f;
-  rx *= lr;
-  ry *= lr;
-  V3 off{c.x_dir[0] * rx + c.y_dir[0] * ry, c.x_dir[1] * rx + c.y_dir[1] * ry,
-         c.x_dir[2] * rx + c.y_dir[2] * ry};
-  r.o = add(loc, off);
-  r.d = normalize_rcp(sub(fp, r.o));
-  return r;
-}
-
-// launch-local pixel index -> image (x, y) and output offset; 8x8 blocks inside tiles so
-// consecutive slots trace spatially coherent rays.
-__device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, int& y, size_t& out_off) {
-  const int tile_px = a.tile_w * a.tile_h;
-  const int tl = (int)fdiv((uint32_t)p, a.fd_tile_px), r = p - tl * tile_px;
-  const int b = r >> 6, l = r & 63;
-  const int by = (int)fdiv((uint32_t)b, a.fd_sub_x), bx = b - by * a.sub_x;
-  const int lx = bx * 8 + (l & 7), ly = by * 8 + (l >> 3);
-  const int tid = a.tile_affine ? a.tile_first + tl * a.tile_step : a.tile_ids[tl];
-  const int ty = (int)fdiv((uint32_t)tid, a.fd_tiles_x), tx = tid - ty * a.tiles_x;
-  x = tx * a.tile_w + lx;
-  y = ty * a.tile_h + ly;
-  const int to = a.tile_out ? a.tile_out[tl] : tl;
-  out_off = ((size_t)to * tile_px + (size_t)ly * a.tile_w + lx) * 3;
-  return x < a.cam.res_x && y < a.cam.res_y;
-}
-
-// ---------------------------------------------------------------- logic kernel
-// unit -> (launch-local pixel, sample); false if the pixel lies outside the image
-__device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, int& px, int& py, int& sample) {
-  // units < 2^31 (checked on the host): 32-bit unsigned division
-  const unsigned u = (unsigned)unit, ns = (unsigned)a.n_samples;
-  const int p = (int)fdiv(u, a.fd_samples);
-  sample = (int)(u - (unsigned)p * ns);
-  size_t off;
-  return pixel_coords(a, p, px, py, off);
-}
-
 // kFrames: some material reflects or refracts (Trace recursion frames needed)
 // kTex: some material has a texture (hit UVs + texel fetch)
 // kPlanes: every primitive is a Plane (no transformed-shape intersection code)
@@ -1679,28 +1724,6 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
       a.wave_done[wave] = no_batch ? 1u : kWaveIdle;
     }
   }
-}
-
-// compute_pixel_color (raytracer.cpp:18-70): the camera ray of sample `sample` of pixel (px,
-// py) -- its RNG stream, the stratified jitter in double, Camera::pixelToRay_thin_lens (the
-// lens draws for an aperture > 0).  The ray's time is the caller's next draw.
-__device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, int sample, Rng& rng) {
-  rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
-  const int s = a.spp_sqrt;
-  float fx, fy;
-  if (s <= 1) {
-    fx = (float)px + 0.5f;
-    fy = (float)py + 0.5f;
-  } else {  // the divisions by s: fast invariant integer division, Markstein quotients (rt_div.h)
-    const int sj = (int)fdiv((uint32_t)sample, a.fd_s), si = sample - sj * s;
-    double ox = rng.next();
-    double oy = rng.next();
-    double sx = rt_div_by((double)si + ox, (double)s, a.inv_s);
-    double sy = rt_div_by((double)sj + oy, (double)s, a.inv_s);
-    fx = (float)((double)px + sx);
-    fy = (float)((double)py + sy);
-  }
-  return camera_ray(a.cam, fx, fy, rng, a.inv_res_x, a.inv_res_y);
 }
 
 // One-pass calls (every sample of the call traced by one launch; no Trace recursion, point
@@ -3155,7 +3178,14 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     P.ta.any_query = aq;
     P.ta.host_flag = s->h_flag;
     P.ta.n_work = (int)n_units;
-    hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
+#if RT_CAM_IN_TRACE
+    P.ta.cam_gen = cam->aperture <= 0.0f ? 1 : 0;
+    P.ta.cam_gen_args = P.la;
+    if (P.ta.cam_gen) {
+      HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)aq, 1, 1, stream), RT_EDEVICE);
+    } else
+#endif
+      hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
     launch_trace(P.ta, p->count_work != 0, planes_only, false, seven, P.trace_blocks, lds, stream);
