@@ -245,6 +245,9 @@ struct LogicArgs {
 #ifndef RT_CAM_IN_TRACE
 #define RT_CAM_IN_TRACE 0
 #endif
+#ifndef RT_NODE_F16
+#define RT_NODE_F16 0
+#endif
 struct TraceArgs {
   Common c;
   const int2* prim_refs;      // (reference index, reference leaf) per primitive
@@ -763,6 +766,41 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
+#if RT_NODE_F16
+  // A/B variant: 80-B device nodes with fp16 plane codes (upload_nodes); v_fma_mix_f32 converts
+  // each code inside its fma -- the same value as the byte convert, so the same bits
+  const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 4);  // entry = node index x 5
+  const float4 g = nd[0];
+  const uint4 px = *reinterpret_cast<const uint4*>(nd + 1);
+  const uint4 py = *reinterpret_cast<const uint4*>(nd + 2);
+  const uint4 pz = *reinterpret_cast<const uint4*>(nd + 3);
+  const int4 qc = *reinterpret_cast<const int4*>(nd + 4);
+  const uint32_t ex = __float_as_uint(g.w);
+  const int cc[4] = {qc.x, qc.y, qc.z, qc.w};
+  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
+  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
+  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
+  // words: (lo01, lo23, hi01, hi23) per axis; perm(hi, lo, sel) is the near pair
+  const uint32_t nx0 = __builtin_amdgcn_perm(px.z, px.x, q.sel[0]), nx1 = __builtin_amdgcn_perm(px.w, px.y, q.sel[0]);
+  const uint32_t fx0 = __builtin_amdgcn_perm(px.x, px.z, q.sel[0]), fx1 = __builtin_amdgcn_perm(px.y, px.w, q.sel[0]);
+  const uint32_t ny0 = __builtin_amdgcn_perm(py.z, py.x, q.sel[1]), ny1 = __builtin_amdgcn_perm(py.w, py.y, q.sel[1]);
+  const uint32_t fy0 = __builtin_amdgcn_perm(py.x, py.z, q.sel[1]), fy1 = __builtin_amdgcn_perm(py.y, py.w, q.sel[1]);
+  const uint32_t nz0 = __builtin_amdgcn_perm(pz.z, pz.x, q.sel[2]), nz1 = __builtin_amdgcn_perm(pz.w, pz.y, q.sel[2]);
+  const uint32_t fz0 = __builtin_amdgcn_perm(pz.x, pz.z, q.sel[2]), fz1 = __builtin_amdgcn_perm(pz.y, pz.w, q.sel[2]);
+  auto lo = [](uint32_t w, float B, float A) {
+    return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu)), B, A);
+  };
+  auto hi = [](uint32_t w, float B, float A) {
+    return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)), B, A);
+  };
+  const float tnx[4] = {lo(nx0, bx, ax), hi(nx0, bx, ax), lo(nx1, bx, ax), hi(nx1, bx, ax)};
+  const float tfx[4] = {lo(fx0, bx, ax), hi(fx0, bx, ax), lo(fx1, bx, ax), hi(fx1, bx, ax)};
+  const float tny[4] = {lo(ny0, by, ay), hi(ny0, by, ay), lo(ny1, by, ay), hi(ny1, by, ay)};
+  const float tfy[4] = {lo(fy0, by, ay), hi(fy0, by, ay), lo(fy1, by, ay), hi(fy1, by, ay)};
+  const float tnz[4] = {lo(nz0, bz, az), hi(nz0, bz, az), lo(nz1, bz, az), hi(nz1, bz, az)};
+  const float tfz[4] = {lo(fz0, bz, az), hi(fz0, bz, az), lo(fz1, bz, az), hi(fz1, bz, az)};
+  const uint32_t meta = (ex >> 24) * 0x00204081u & 0x01010101u;  // count_work: valid mask bit k -> byte k
+#else
   const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
   const float4 g = nd[0];
   const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
@@ -787,8 +825,9 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   const float tfy[4] = {pl(fyw, 0, by, ay), pl(fyw, 1, by, ay), pl(fyw, 2, by, ay), pl(fyw, 3, by, ay)};
   const float tnz[4] = {pl(nzw, 0, bz, az), pl(nzw, 1, bz, az), pl(nzw, 2, bz, az), pl(nzw, 3, bz, az)};
   const float tfz[4] = {pl(fzw, 0, bz, az), pl(fzw, 1, bz, az), pl(fzw, 2, bz, az), pl(fzw, 3, bz, az)};
+  const uint32_t meta = qb.z;
+#endif
   if (kCount) {
-    const uint32_t meta = qb.z;
     const uint64_t wm = __ballot(1);
     if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
     ++nvisit;
@@ -2385,9 +2424,51 @@ static int upload(void** dst, const void* src, size_t bytes) {
 
 // The 64-B nodes as laid out in HBM: AoS, one node = four consecutive 16-B words fetched by
 // one lane (an SoA layout -- word k of every node in array k -- measured 2.3 % slower, r04).
+#if RT_NODE_F16
+// A/B variant: 80-B device nodes -- origin + exponents (valid-child mask in the top byte),
+// per axis the words (lo01, lo23, hi01, hi23) of fp16 plane codes (exact: codes < 256), the
+// child entries with internal children as node index x 5 (the node's byte offset / 16)
+struct NodeF16 {
+  float origin[3];
+  uint32_t exps;
+  uint32_t p[3][4];
+  int32_t child[4];
+};
+static_assert(sizeof(NodeF16) == 80, "80-B device node");
+static uint32_t f16_code(uint32_t c) {  // binary16 bits of the integer c < 2048
+  if (c == 0) return 0;
+  int e = 31 - __builtin_clz(c);
+  return (uint32_t)(e + 15) << 10 | ((c << (10 - e)) & 0x3ffu);
+}
+static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
+  std::vector<NodeF16> v((size_t)n);
+  for (int32_t i = 0; i < n; ++i) {
+    const rt_node4& s = nodes[i];
+    NodeF16& d = v[(size_t)i];
+    uint32_t valid = 0;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t m = (s.meta >> (8 * k)) & 0xffu;
+      if (m) valid |= 1u << k;
+      d.child[k] = m == 0x01u ? s.child[k] * 5 : s.child[k];
+    }
+    for (int a = 0; a < 3; ++a) d.origin[a] = s.origin[a];
+    d.exps = (s.exps & 0xffffffu) | valid << 24;
+    const uint32_t qlo[3] = {s.q_lo_x, s.q_lo_y, s.q_lo_z}, qhi[3] = {s.q_hi_x, s.q_hi_y, s.q_hi_z};
+    for (int a = 0; a < 3; ++a) {
+      auto pair = [](uint32_t w, int k) { return f16_code((w >> (8 * k)) & 0xffu) | f16_code((w >> (8 * k + 8)) & 0xffu) << 16; };
+      d.p[a][0] = pair(qlo[a], 0);
+      d.p[a][1] = pair(qlo[a], 2);
+      d.p[a][2] = pair(qhi[a], 0);
+      d.p[a][3] = pair(qhi[a], 2);
+    }
+  }
+  return upload(dst, v.data(), v.size() * sizeof(NodeF16));
+}
+#else
 static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
   return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
 }
+#endif
 
 int rt_scene_destroy(rt_scene_t s) {
   if (!s) return RT_OK;

@@ -101,6 +101,21 @@ __global__ __launch_bounds__(256) void spin(float* out, float seed) {
       }
       if (KIND == 50) { U1("v_sub_u32 %0, %0, %1"); U1("v_ashrrev_i32 %0, 31, %0"); U1("v_or_b32 %0, %0, %1"); }
       if (KIND == 51) U1("v_ashrrev_i32 %0, 31, %0");
+      // fp16 plane codes: v_fma_mix_f32 converts its f16 operand (either half) inside the fma
+#define MIX(sel) asm volatile("v_fma_mix_f32 %0, %1, %0, %2 " sel : "+v"(x[k]) : "v"(u[k]), "v"(z[k]))
+      if (KIND == 52) MIX("op_sel_hi:[1,0,0]");
+      if (KIND == 53) MIX("op_sel:[1,0,0] op_sel_hi:[1,0,0]");
+      if (KIND == 54) { MIX("op_sel_hi:[1,0,0]"); U1("v_max3_i32 %0, %0, %1, %2"); }
+      if (KIND == 55) { MIX("op_sel_hi:[1,0,0]"); U1("v_perm_b32 %0, %0, %1, %2"); }
+      if (KIND == 56) { MIX("op_sel_hi:[1,0,0]"); U1("v_add_u32 %0, %0, %1"); }
+      if (KIND == 57) { MIX("op_sel_hi:[1,0,0]"); asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(y[k]) : "v"(v[k])); }
+      if (KIND == 58) { MIX("op_sel_hi:[1,0,0]"); A1("v_fma_f32 %0, %0, %1, %2"); }
+      if (KIND == 59) {  // f16 plane pairs selected by perm: one perm, two mixed fmas per child-axis pair
+        U1("v_perm_b32 %0, %0, %1, %2");
+        MIX("op_sel_hi:[1,0,0]");
+        MIX("op_sel:[1,0,0] op_sel_hi:[1,0,0]");
+      }
+#undef MIX
     }
   }
   float s = 0;
@@ -186,5 +201,13 @@ int main() {
   run<49>("bytes: 0.5 perm+2 cvt+2 fma", 4.5, ncu);
   run<50>("sub_u32 + ashr + or (cull mask)", 3, ncu);
   run<51>("v_ashrrev_i32", 1, ncu);
+  run<52>("v_fma_mix_f32 (lo half)", 1, ncu);
+  run<53>("v_fma_mix_f32 (hi half)", 1, ncu);
+  run<54>("fma_mix + max3_i32", 2, ncu);
+  run<55>("fma_mix + perm", 2, ncu);
+  run<56>("fma_mix + add_u32", 2, ncu);
+  run<57>("fma_mix + cvt_f32_ubyte1", 2, ncu);
+  run<58>("fma_mix + fma_f32", 2, ncu);
+  run<59>("f16 pair: perm + 2 fma_mix", 3, ncu);
   return 0;
 }
