@@ -242,12 +242,6 @@ struct LogicArgs {
   int op_fo, op_ft, op_fk;
 };
 
-#ifndef RT_CAM_IN_TRACE
-#define RT_CAM_IN_TRACE 0
-#endif
-#ifndef RT_NODE_F16
-#define RT_NODE_F16 0
-#endif
 struct TraceArgs {
   Common c;
   const int2* prim_refs;      // (reference index, reference leaf) per primitive
@@ -297,13 +291,6 @@ struct TraceArgs {
   // their tiles by
   unsigned int* tile_cost;
   FastDiv fd_tile_units;
-#if RT_CAM_IN_TRACE
-  // A/B variant: pinhole one-pass calls generate each unit's camera ray
-  // at refill (sample_ray on this copy of the call's LogicArgs) instead of reading camera_kernel's
-  // query record (skipping that kernel and its 12 B per unit of writes and reads)
-  LogicArgs cam_gen_args;
-  int cam_gen;
-#endif
 #ifdef RT_EXIT_TIMING
   unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
 #endif
@@ -542,19 +529,6 @@ __device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, in
 
 // Reads slot's query record; false if the slot emitted no query this step.
 __device__ __forceinline__ bool begin_query(const TraceArgs& a, int slot, Query& q) {
-#if RT_CAM_IN_TRACE
-  if (a.cam_gen) {  // the unit's camera ray, generated here (camera_kernel's ops)
-    int px, py, sample;
-    if (!unit_coords(a.cam_gen_args, (long long)(unsigned)slot, px, py, sample)) {
-      a.result[slot] = -1;
-      return false;
-    }
-    Rng rng;
-    const Ray ray = sample_ray(a.cam_gen_args, px, py, sample, rng);
-    setup_query(q, ray.o, ray.d, a.op_ft >= 0 ? (float)rng.next() : 0.0f, false);
-    return true;
-  }
-#endif
   if (a.one_pass) {  // the unit's camera ray (camera_kernel): 64-bit field offsets (up to 2^30 slots)
     const size_t n = (size_t)(unsigned)a.n_slots, u = (size_t)(unsigned)slot;
     if (a.op_fk >= 0 && __float_as_int(a.query[(size_t)a.op_fk * n + u]) < 0) return false;
@@ -760,73 +734,82 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
 // always miss; child entries come precomputed from the host (node index, or the encoded
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
-template <bool kCount>
+template <bool kCount, bool kF16>
 __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, float lim, int node,
                                           const LaneStack& S, int& w, int gtid, unsigned int& nbox,
                                           unsigned long long& dg_any_box, unsigned int& nvisit) {
   const Ray& r = q.r;
   const V3& inv = q.inv;
-#if RT_NODE_F16
-  // A/B variant: 80-B device nodes with fp16 plane codes (upload_nodes); v_fma_mix_f32 converts
-  // each code inside its fma -- the same value as the byte convert, so the same bits
-  const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 4);  // entry = node index x 5
-  const float4 g = nd[0];
-  const uint4 px = *reinterpret_cast<const uint4*>(nd + 1);
-  const uint4 py = *reinterpret_cast<const uint4*>(nd + 2);
-  const uint4 pz = *reinterpret_cast<const uint4*>(nd + 3);
-  const int4 qc = *reinterpret_cast<const int4*>(nd + 4);
-  const uint32_t ex = __float_as_uint(g.w);
-  const int cc[4] = {qc.x, qc.y, qc.z, qc.w};
-  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
-  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
-  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
-  // words: (lo01, lo23, hi01, hi23) per axis; perm(hi, lo, sel) is the near pair
-  const uint32_t nx0 = __builtin_amdgcn_perm(px.z, px.x, q.sel[0]), nx1 = __builtin_amdgcn_perm(px.w, px.y, q.sel[0]);
-  const uint32_t fx0 = __builtin_amdgcn_perm(px.x, px.z, q.sel[0]), fx1 = __builtin_amdgcn_perm(px.y, px.w, q.sel[0]);
-  const uint32_t ny0 = __builtin_amdgcn_perm(py.z, py.x, q.sel[1]), ny1 = __builtin_amdgcn_perm(py.w, py.y, q.sel[1]);
-  const uint32_t fy0 = __builtin_amdgcn_perm(py.x, py.z, q.sel[1]), fy1 = __builtin_amdgcn_perm(py.y, py.w, q.sel[1]);
-  const uint32_t nz0 = __builtin_amdgcn_perm(pz.z, pz.x, q.sel[2]), nz1 = __builtin_amdgcn_perm(pz.w, pz.y, q.sel[2]);
-  const uint32_t fz0 = __builtin_amdgcn_perm(pz.x, pz.z, q.sel[2]), fz1 = __builtin_amdgcn_perm(pz.y, pz.w, q.sel[2]);
-  auto lo = [](uint32_t w, float B, float A) {
-    return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu)), B, A);
+  float tnx[4], tfx[4], tny[4], tfy[4], tnz[4], tfz[4];
+  int cc[4];
+  uint32_t meta;  // count_work: byte k nonzero for a child in slot k
+  auto g_terms = [&](const float4 g, float& ax, float& bx, float& ay, float& by, float& az, float& bz) {
+    const uint32_t ex = __float_as_uint(g.w);
+    ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
+    ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
+    az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
   };
-  auto hi = [](uint32_t w, float B, float A) {
-    return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)), B, A);
-  };
-  const float tnx[4] = {lo(nx0, bx, ax), hi(nx0, bx, ax), lo(nx1, bx, ax), hi(nx1, bx, ax)};
-  const float tfx[4] = {lo(fx0, bx, ax), hi(fx0, bx, ax), lo(fx1, bx, ax), hi(fx1, bx, ax)};
-  const float tny[4] = {lo(ny0, by, ay), hi(ny0, by, ay), lo(ny1, by, ay), hi(ny1, by, ay)};
-  const float tfy[4] = {lo(fy0, by, ay), hi(fy0, by, ay), lo(fy1, by, ay), hi(fy1, by, ay)};
-  const float tnz[4] = {lo(nz0, bz, az), hi(nz0, bz, az), lo(nz1, bz, az), hi(nz1, bz, az)};
-  const float tfz[4] = {lo(fz0, bz, az), hi(fz0, bz, az), lo(fz1, bz, az), hi(fz1, bz, az)};
-  const uint32_t meta = (ex >> 24) * 0x00204081u & 0x01010101u;  // count_work: valid mask bit k -> byte k
-#else
-  const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
-  const float4 g = nd[0];
-  const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
-  const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
-  const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
-  const uint32_t ex = __float_as_uint(g.w);
-  const int cc[4] = {(int)qb.w, qc.x, qc.y, qc.z};
-  const float ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
-  const float ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
-  const float az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
-  // perm(hi, lo, sel) is the near word; swapping the operands gives the far one
-  const uint32_t nxw = __builtin_amdgcn_perm(qa.y, qa.x, q.sel[0]), fxw = __builtin_amdgcn_perm(qa.x, qa.y, q.sel[0]);
-  const uint32_t nyw = __builtin_amdgcn_perm(qa.w, qa.z, q.sel[1]), fyw = __builtin_amdgcn_perm(qa.z, qa.w, q.sel[1]);
-  const uint32_t nzw = __builtin_amdgcn_perm(qb.y, qb.x, q.sel[2]), fzw = __builtin_amdgcn_perm(qb.x, qb.y, q.sel[2]);
-  // one v_fma_f32 per plane: on gfx950 it issues beside the byte converts, where a v_pk_fma_f32
-  // (two planes) does not (tools/ubench_mix.hip; r05 A/B: headline +2.5 %, one rank's eighth
-  // +2.6 %, C5 +3.6 %; the same fma per plane, so the same bits)
-  auto pl = [](uint32_t w, int k, float B, float A) { return __builtin_fmaf((float)((w >> (8 * k)) & 0xffu), B, A); };
-  const float tnx[4] = {pl(nxw, 0, bx, ax), pl(nxw, 1, bx, ax), pl(nxw, 2, bx, ax), pl(nxw, 3, bx, ax)};
-  const float tfx[4] = {pl(fxw, 0, bx, ax), pl(fxw, 1, bx, ax), pl(fxw, 2, bx, ax), pl(fxw, 3, bx, ax)};
-  const float tny[4] = {pl(nyw, 0, by, ay), pl(nyw, 1, by, ay), pl(nyw, 2, by, ay), pl(nyw, 3, by, ay)};
-  const float tfy[4] = {pl(fyw, 0, by, ay), pl(fyw, 1, by, ay), pl(fyw, 2, by, ay), pl(fyw, 3, by, ay)};
-  const float tnz[4] = {pl(nzw, 0, bz, az), pl(nzw, 1, bz, az), pl(nzw, 2, bz, az), pl(nzw, 3, bz, az)};
-  const float tfz[4] = {pl(fzw, 0, bz, az), pl(fzw, 1, bz, az), pl(fzw, 2, bz, az), pl(fzw, 3, bz, az)};
-  const uint32_t meta = qb.z;
-#endif
+  float ax, bx, ay, by, az, bz;
+  if constexpr (kF16) {
+    // planes-only scenes: 80-B device nodes with fp16 plane codes (upload_nodes); v_fma_mix_f32
+    // converts each code inside its fma -- the value the byte convert gives, so the same bits --
+    // and takes the 24 byte converts out of the visit (r05 A/B, same box: headline +2.9 %, one
+    // rank's eighth +2.3 %, C5 +3.6 %; the code pairs picked by a per-lane load address
+    // instead of the perms: -13 %, eight loads per visit).  Transformed-shape instances keep the
+    // byte codes: there the wider node cost 10 more spilled VGPRs (C3 -4.5 %).
+    const char* nb = reinterpret_cast<const char*>(a.c.nodes) + ((uint32_t)node << 4);  // entry = node index x 5
+    const float4 g = *reinterpret_cast<const float4*>(nb);
+    const int4 qc = *reinterpret_cast<const int4*>(nb + 64);
+    uint32_t nx0, nx1, fx0, fx1, ny0, ny1, fy0, fy1, nz0, nz1, fz0, fz1;
+    // words (lo01, lo23, hi01, hi23) per axis; perm(hi, lo, sel) is the near pair
+    const uint4 px = *reinterpret_cast<const uint4*>(nb + 16);
+    const uint4 py = *reinterpret_cast<const uint4*>(nb + 32);
+    const uint4 pz = *reinterpret_cast<const uint4*>(nb + 48);
+    nx0 = __builtin_amdgcn_perm(px.z, px.x, q.sel[0]), nx1 = __builtin_amdgcn_perm(px.w, px.y, q.sel[0]);
+    fx0 = __builtin_amdgcn_perm(px.x, px.z, q.sel[0]), fx1 = __builtin_amdgcn_perm(px.y, px.w, q.sel[0]);
+    ny0 = __builtin_amdgcn_perm(py.z, py.x, q.sel[1]), ny1 = __builtin_amdgcn_perm(py.w, py.y, q.sel[1]);
+    fy0 = __builtin_amdgcn_perm(py.x, py.z, q.sel[1]), fy1 = __builtin_amdgcn_perm(py.y, py.w, q.sel[1]);
+    nz0 = __builtin_amdgcn_perm(pz.z, pz.x, q.sel[2]), nz1 = __builtin_amdgcn_perm(pz.w, pz.y, q.sel[2]);
+    fz0 = __builtin_amdgcn_perm(pz.x, pz.z, q.sel[2]), fz1 = __builtin_amdgcn_perm(pz.y, pz.w, q.sel[2]);
+    g_terms(g, ax, bx, ay, by, az, bz);
+    cc[0] = qc.x, cc[1] = qc.y, cc[2] = qc.z, cc[3] = qc.w;
+    auto lo = [](uint32_t w, float B, float A) {
+      return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu)), B, A);
+    };
+    auto hi = [](uint32_t w, float B, float A) {
+      return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)), B, A);
+    };
+    tnx[0] = lo(nx0, bx, ax), tnx[1] = hi(nx0, bx, ax), tnx[2] = lo(nx1, bx, ax), tnx[3] = hi(nx1, bx, ax);
+    tfx[0] = lo(fx0, bx, ax), tfx[1] = hi(fx0, bx, ax), tfx[2] = lo(fx1, bx, ax), tfx[3] = hi(fx1, bx, ax);
+    tny[0] = lo(ny0, by, ay), tny[1] = hi(ny0, by, ay), tny[2] = lo(ny1, by, ay), tny[3] = hi(ny1, by, ay);
+    tfy[0] = lo(fy0, by, ay), tfy[1] = hi(fy0, by, ay), tfy[2] = lo(fy1, by, ay), tfy[3] = hi(fy1, by, ay);
+    tnz[0] = lo(nz0, bz, az), tnz[1] = hi(nz0, bz, az), tnz[2] = lo(nz1, bz, az), tnz[3] = hi(nz1, bz, az);
+    tfz[0] = lo(fz0, bz, az), tfz[1] = hi(fz0, bz, az), tfz[2] = lo(fz1, bz, az), tfz[3] = hi(fz1, bz, az);
+    meta = (__float_as_uint(g.w) >> 24) * 0x00204081u & 0x01010101u;  // valid mask bit k -> byte k
+  } else {
+    const float4* nd = at_byte(a.c.nodes, (uint32_t)node << 6);  // node < 2^26 (rt_scene_create)
+    const float4 g = nd[0];
+    const uint4 qa = *reinterpret_cast<const uint4*>(nd + 1);
+    const uint4 qb = *reinterpret_cast<const uint4*>(nd + 2);
+    const int4 qc = *reinterpret_cast<const int4*>(nd + 3);
+    cc[0] = (int)qb.w, cc[1] = qc.x, cc[2] = qc.y, cc[3] = qc.z;
+    g_terms(g, ax, bx, ay, by, az, bz);
+    // perm(hi, lo, sel) is the near word; swapping the operands gives the far one
+    const uint32_t nxw = __builtin_amdgcn_perm(qa.y, qa.x, q.sel[0]), fxw = __builtin_amdgcn_perm(qa.x, qa.y, q.sel[0]);
+    const uint32_t nyw = __builtin_amdgcn_perm(qa.w, qa.z, q.sel[1]), fyw = __builtin_amdgcn_perm(qa.z, qa.w, q.sel[1]);
+    const uint32_t nzw = __builtin_amdgcn_perm(qb.y, qb.x, q.sel[2]), fzw = __builtin_amdgcn_perm(qb.x, qb.y, q.sel[2]);
+    // one v_fma_f32 per plane: on gfx950 it issues beside the byte converts, where a v_pk_fma_f32
+    // (two planes) does not (tools/ubench_mix.hip; r05 A/B: headline +2.5 %, one rank's eighth
+    // +2.6 %, C5 +3.6 %; the same fma per plane, so the same bits)
+    auto pl = [](uint32_t w, int k, float B, float A) { return __builtin_fmaf((float)((w >> (8 * k)) & 0xffu), B, A); };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      tnx[k] = pl(nxw, k, bx, ax), tfx[k] = pl(fxw, k, bx, ax);
+      tny[k] = pl(nyw, k, by, ay), tfy[k] = pl(fyw, k, by, ay);
+      tnz[k] = pl(nzw, k, bz, az), tfz[k] = pl(fzw, k, bz, az);
+    }
+    meta = qb.z;
+  }
   if (kCount) {
     const uint64_t wm = __ballot(1);
     if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
@@ -1227,11 +1210,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
 #ifdef RT_PHASE_TIMING
     if (const uint64_t nm = __ballot(item >= 0)) {
       RT_PT_LANES(2, (unsigned long long)__popcll(nm), 64ull);
-      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
+      if (item >= 0) item = node_visit<kCount, kPlanesOnly>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
       RT_PT_MARK(2);  // node phase
     }
 #else
-    if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
+    if (item >= 0) item = node_visit<kCount, kPlanesOnly>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
 #endif
   }
   // ---- drain (drain_help: the queue is dry).  A query still traversing keeps its lane (its
@@ -1345,7 +1328,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           item = h.done ? kNoItem : stack_pop_live(a, S, sw, gtid, lim);
         }
       }
-      if (item >= 0) item = node_visit<kCount>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
+      if (item >= 0) item = node_visit<kCount, kPlanesOnly>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
     }
   }
   RT_PT_FLUSH
@@ -2422,12 +2405,12 @@ static int upload(void** dst, const void* src, size_t bytes) {
   return RT_OK;
 }
 
-// The 64-B nodes as laid out in HBM: AoS, one node = four consecutive 16-B words fetched by
-// one lane (an SoA layout -- word k of every node in array k -- measured 2.3 % slower, r04).
-#if RT_NODE_F16
-// A/B variant: 80-B device nodes -- origin + exponents (valid-child mask in the top byte),
-// per axis the words (lo01, lo23, hi01, hi23) of fp16 plane codes (exact: codes < 256), the
-// child entries with internal children as node index x 5 (the node's byte offset / 16)
+// The nodes as laid out in HBM: AoS, one node = consecutive 16-B words fetched by one lane (an
+// SoA layout -- word k of every node in array k -- measured 2.3 % slower, r04).  Scenes with
+// transformed shapes keep the 64-B rt_node4 records; planes-only scenes get 80-B device nodes
+// -- origin + exponents (valid-child mask in the top byte), per axis the words (lo01, lo23,
+// hi01, hi23) of fp16 plane codes (exact: codes < 256), the child entries with internal
+// children as node index x 5 (the node's byte offset / 16) -- for node_visit's mixed fmas
 struct NodeF16 {
   float origin[3];
   uint32_t exps;
@@ -2440,7 +2423,8 @@ static uint32_t f16_code(uint32_t c) {  // binary16 bits of the integer c < 2048
   int e = 31 - __builtin_clz(c);
   return (uint32_t)(e + 15) << 10 | ((c << (10 - e)) & 0x3ffu);
 }
-static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
+static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n, bool planes_only) {
+  if (!planes_only) return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
   std::vector<NodeF16> v((size_t)n);
   for (int32_t i = 0; i < n; ++i) {
     const rt_node4& s = nodes[i];
@@ -2464,11 +2448,6 @@ static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
   }
   return upload(dst, v.data(), v.size() * sizeof(NodeF16));
 }
-#else
-static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n) {
-  return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
-}
-#endif
 
 int rt_scene_destroy(rt_scene_t s) {
   if (!s) return RT_OK;
@@ -2561,7 +2540,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
   int rc = RT_OK;
   if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
-      (rc = upload_nodes(&s->d_nodes, d->nodes, d->n_nodes)) ||
+      (rc = upload_nodes(&s->d_nodes, d->nodes, d->n_nodes, d->prim_stride == 64)) ||
       (rc = upload(&s->d_prim_refs, d->prim_refs, (size_t)d->n_prims * sizeof(rt_prim_ref))) ||
       (rc = upload(&s->d_ref_boxes, d->ref_leaf_boxes, (size_t)d->n_ref_leaves * 8 * sizeof(float))) ||
       (rc = upload(&s->d_mats, d->materials, (size_t)d->n_materials * sizeof(rt_material))) ||
@@ -3259,14 +3238,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     P.ta.any_query = aq;
     P.ta.host_flag = s->h_flag;
     P.ta.n_work = (int)n_units;
-#if RT_CAM_IN_TRACE
-    P.ta.cam_gen = cam->aperture <= 0.0f ? 1 : 0;
-    P.ta.cam_gen_args = P.la;
-    if (P.ta.cam_gen) {
-      HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)aq, 1, 1, stream), RT_EDEVICE);
-    } else
-#endif
-      hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
+    hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
     launch_trace(P.ta, p->count_work != 0, planes_only, false, seven, P.trace_blocks, lds, stream);

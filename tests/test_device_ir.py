@@ -36,14 +36,15 @@ def test_no_approximate_div_sqrt(ir):
 
 
 def _culling_fmas(ir: str) -> tuple[int, int]:
-    """(scalar f32 fmas whose first operand is a converted integer -- the BVH slab test's
-    `fma(float(code), step * inv, (origin - o) * inv)`, node_visit -- , all scalar f32 fmas)."""
+    """(scalar f32 fmas whose first operand is a converted plane code -- the BVH slab test's
+    `fma(float(code), step * inv, (origin - o) * inv)`, node_visit: a byte code (uitofp) or, in
+    planes-only instances, an fp16 code (fpext half) -- , all scalar f32 fmas)."""
     import re
     conv, cull, total = set(), 0, 0
     for line in ir.splitlines():
         if line.startswith("define "):
             conv = set()  # value names are per function
-        m = re.match(r"\s*(%[\w.]+) = uitofp ", line)
+        m = re.match(r"\s*(%[\w.]+) = (uitofp|fpext half) ", line)
         if m:
             conv.add(m.group(1))
         if re.search(r"call (noundef )?float @llvm\.fma\.f32\(float ", line):
@@ -59,7 +60,8 @@ def test_fma_only_in_powf_div_and_culling(ir):
     # Markstein quotient (rt_div.h: exact remainder and correction, == IEEE division,
     # tests/test_div.py), and the fma of the BVH slab test, which only culls (padded boxes, exact
     # re-check of every candidate hit) -- one scalar fma per plane (r05: it issues beside the
-    # byte converts; a packed fma does not), recognised by its converted-code first operand.
+    # byte converts; a packed fma does not), recognised by its converted-code first operand
+    # (a byte, or the fp16 code v_fma_mix_f32 converts inside the fma).
     # Every other scalar f32 fma is one of rt_div_by's two, whose first takes an fneg (the
     # remainder's -q0); CSE may merge one of a pair across identical quotients, so the count
     # need not be even.
