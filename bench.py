@@ -23,8 +23,8 @@ build) over 256 CUs x the highest wave64 VALU issue rate per CU-cycle that SQ_IN
 shows for tools/ubench_valu.hip's instruction streams (1.73, a mixed int / convert / fp32
 stream; the guide's spec 2 per CU-cycle beside it) x 2.4 GHz.  Beside it, per average trace launch (HIP
 events on the launch stream over the timed steps): `hbm` = PMC HBM bytes (traffic) / launch
-time vs 8 TB/s, and `l2` = algorithmic bytes (64 B per BVH4 node visit + 64 B per primitive
-test, counted by an instrumented run of the same frame) / launch time vs the L2's 34.5 TB/s.
+time vs 8 TB/s, and `l2` = algorithmic bytes (80 B per BVH4 node visit in planes-only scenes,
+64 B otherwise, + the primitive record per primitive test, counted by an instrumented run of the same frame) / launch time vs the L2's 34.5 TB/s.
 Scenes of a few primitives (C1-C4) get no roofline claim.
 cpu_baseline: the compiled reference (oracle/_ref/ref_driver; kind "reference") -- or the
 oracle restatement if the reference binary is absent (kind "port") -- on rank 0 at N=1,
@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 #     4 SIMDs per CU = 2 instructions per CU-cycle (78.6 T lane-ops/s)
 N_CU, MAX_CLOCK_GHZ = 256, 2.4
 SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE = 2.0
-UBENCH_PROFILE = "r04_v3"  # committed counter-measured VALU microbenchmark (profiles/)
+UBENCH_PROFILE = "r05_v1"  # committed counter-measured VALU microbenchmark (profiles/)
 
 
 def valu_peak(path):
@@ -66,8 +66,10 @@ def valu_peak(path):
         if d.get("max_valu_wave_instr_per_cu_cycle"):
             return float(d["max_valu_wave_instr_per_cu_cycle"]), f"{os.path.relpath(path, ROOT)} ({d.get('label', '')})"
     return 1.0, "assumed 1 wave64 instruction per CU-cycle (no counter-measured microbenchmark found)"
-NODE_BYTES, PRIM_BYTES = 64, 64  # one 64-B BVH4 node per visit; one 64-B plane record per test
-PMC_PROFILE = "r04_v3"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+# one BVH4 node per visit: 80 B in planes-only scenes (fp16 plane codes), 64 B otherwise;
+# one 64-B plane / 128-B transformed record per primitive test
+NODE_BYTES_PLANES, NODE_BYTES_OTHER = 80, 64
+PMC_PROFILE = "r05_v1"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
@@ -481,7 +483,8 @@ def main():
                          count_work=True)
     cst = ds.render_tiles(mine, T, T, out.data_ptr(), cp)
     prim_bytes = scene.info.prim_stride  # 64 B planes / 128 B transformed records
-    bytes_per_ray = (NODE_BYTES * cst.node_visits + prim_bytes * cst.prim_tests) / max(cst.rays, 1)
+    node_bytes = NODE_BYTES_PLANES if prim_bytes == 64 else NODE_BYTES_OTHER
+    bytes_per_ray = (node_bytes * cst.node_visits + prim_bytes * cst.prim_tests) / max(cst.rays, 1)
     log(f"[rank {rank}] instrumented: rays {cst.rays}, node visits {cst.node_visits} "
         f"({cst.node_visits / max(cst.rays, 1):.2f}/ray), box tests {cst.box_tests} "
         f"({cst.box_tests / max(cst.rays, 1):.1f}/ray), prim tests {cst.prim_tests} "
@@ -674,7 +677,7 @@ def main():
                             "bytes, and the north_star's HBM-read target does not apply at this working set; the "
                             "binding roof is VALU issue (frac above)"},
             "l2": {"alg_bytes_per_launch": int(avg_launch_bytes), "alg_bytes_per_ray": round(bytes_per_ray, 1),
-                   "model": "64 B per BVH4 node visit + prim_stride B per primitive test",
+                   "model": "80 B (planes-only scenes: fp16 plane codes) / 64 B per BVH4 node visit + prim_stride B per primitive test",
                    "achieved_gbs_per_launch": round(alg_rate, 1),
                    "achieved_gbs": round(alg_rate_busy, 1) if alg_rate_busy else None, "peak_gbs": L2_PEAK_GBS,
                    "frac": round(alg_rate_busy / L2_PEAK_GBS, 4) if alg_rate_busy else None},
