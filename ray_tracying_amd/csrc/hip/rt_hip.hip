@@ -58,6 +58,15 @@ constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 
 constexpr int kFetchStride = 32;      // u32 words between counters
 constexpr int kCtlBytes = 4096;    // control block (cleared by init_kernel)
 constexpr int kStatsBytes = 512;
+// RT_WRITE_DIAG (diagnostic builds only): counts the traversal's HBM stores by kind -- stack
+// entries past the LDS rows (8 B), result words (4 B), hit records (32 B), occlusion words (4 B)
+// -- into control-block counters 80..83, printed per one-pass call (the PMC WRITE_SIZE
+// attribution)
+#ifdef RT_WRITE_DIAG
+#define RT_WD(k) atomicAdd(a.counters + 80 + (k), 1ull)
+#else
+#define RT_WD(k)
+#endif
 // scenes with fewer primitives spend their frame in the per-step passes over the slots, not in
 // traversal: their shadow rays are fused whatever the call size
 constexpr int kFuseFewPrims = 65536;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
@@ -572,7 +581,9 @@ __device__ __forceinline__ bool finish_query(const TraceArgs& a, int slot, const
   const Ray& r = q.r;
   complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
   a.result[slot] = q.any ? (h.done ? 1 : 0) : h.best_idx;
+  RT_WD(1);
   if (kPlanesOnly && !a.has_tex && !q.any && h.best_idx >= 0) {
+    RT_WD(2);
     const float4* rec = at_byte(a.c.prims, (uint32_t)h.best_idx * ((uint32_t)a.c.prim_stride4 << 4));  // < 2^24
     const float* w = reinterpret_cast<const float*>(rec);
     hn = V3{w[3], w[7], w[11]};
@@ -683,8 +694,12 @@ __device__ __forceinline__ int2* stack_at(const TraceArgs& a, const LaneStack& S
 
 __device__ __forceinline__ void stack_push(const TraceArgs& a, const LaneStack& S, int& w, int gtid, int e, float t) {
   const int sp = stack_depth(w);
-  if (sp < a.lds_entries) *reinterpret_cast<int2*>(S.lds + w) = make_int2(e, __float_as_int(t));
-  else S.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = make_int2(e, __float_as_int(t));
+  if (sp < a.lds_entries) {
+    *reinterpret_cast<int2*>(S.lds + w) = make_int2(e, __float_as_int(t));
+  } else {
+    S.spill[(size_t)(sp - a.lds_entries) * a.n_threads + gtid] = make_int2(e, __float_as_int(t));
+    RT_WD(0);
+  }
   w += kStackRow;
 }
 
@@ -714,7 +729,10 @@ __device__ __forceinline__ int stack_pop_live(const TraceArgs& a, const LaneStac
 __device__ __forceinline__ int2 stack_take_bottom(const TraceArgs& a, const LaneStack& S, int& w, int gtid) {
   const int col = stack_empty_word(w), sp = stack_depth(w);
   const int2 b = *stack_at(a, S, col, 0, gtid);
-  for (int i = 1; i < sp; ++i) *stack_at(a, S, col, i - 1, gtid) = *stack_at(a, S, col, i, gtid);
+  for (int i = 1; i < sp; ++i) {
+    *stack_at(a, S, col, i - 1, gtid) = *stack_at(a, S, col, i, gtid);
+    if (i - 1 >= a.lds_entries) RT_WD(0);
+  }
   w -= kStackRow;
   return b;
 }
@@ -1082,6 +1100,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         next = l + 1;
       } else {
         a.occl[slot] = bits;
+        RT_WD(3);
         fz = 0;
       }
     } else {
@@ -2280,7 +2299,7 @@ struct rt_scene_s {
     int n_tiles = 0, tiles_x = 0, tiles_y = 0;
     std::vector<int32_t> tl_dev;
     std::vector<unsigned char> meas_key;
-#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING)
+#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING) || defined(RT_WRITE_DIAG)
     TraceArgs ta{};
 #endif
   } pending;
@@ -2698,6 +2717,15 @@ static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
 #endif
 #ifdef RT_PHASE_TIMING
   if (const int rc = print_phase_timing(q.ta.counters)) return rc;
+#endif
+#ifdef RT_WRITE_DIAG
+  {
+    unsigned long long wd[4] = {};
+    HIP_TRY(hipMemcpy(wd, q.ta.counters + 80, sizeof(wd), hipMemcpyDeviceToHost), RT_EDEVICE);
+    std::fprintf(stderr, "[rt writes] HBM stack entries %llu (%.3f GB), result words %llu (%.3f GB), hit records %llu "
+                 "(%.3f GB), occlusion words %llu (%.3f GB)\n", wd[0], wd[0] * 8e-9, wd[1], wd[1] * 4e-9, wd[2],
+                 wd[2] * 32e-9, wd[3], wd[3] * 4e-9);
+  }
 #endif
   s->last_iters = 1;
   if (!stats) return RT_OK;
@@ -3262,7 +3290,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     q.tiles_y = tiles_y;
     q.tl_dev = tl_dev;
     q.meas_key = meas_key_of(cam, tile_w, tile_h, n_samples);
-#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING)
+#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING) || defined(RT_WRITE_DIAG)
     q.ta = P.ta;
 #endif
     // sync == 0: deferred -- rt_render_wait (or the scene's next call) finishes it, so the
