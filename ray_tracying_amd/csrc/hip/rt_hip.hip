@@ -251,6 +251,9 @@ struct LogicArgs {
   int op_fo, op_ft, op_fk;
 };
 
+#ifndef RT_XCD_CHUNK_DEFAULT
+#define RT_XCD_CHUNK_DEFAULT 64  // r05 A/B (same box, 3 reps interleaved): headline +0.9 %, one rank's eighth +0.4 %, C5 +-0
+#endif
 struct TraceArgs {
   Common c;
   const int2* prim_refs;      // (reference index, reference leaf) per primitive
@@ -261,6 +264,7 @@ struct TraceArgs {
   int* result;
   unsigned int* fetch;        // fetch_shards work counters over slot slices (zeroed per step)
   int fetch_shards;
+  int xcd_chunk;              // > 0: XCD-aware deal of chunks of this many groups (fetch loop)
   const unsigned int* any_query;  // logic's "some slot has a query" flag for this step
   float cam_loc[3];           // origin of the queries marked kQueryCamOrigin
   unsigned int* host_flag;    // pinned host word: any_query of this step, for the host's loop
@@ -974,6 +978,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   // shard g % shards), so the queue is consumed in slot order -- the call's costliest tiles
   // first (tile_cost_order) -- and the launch ends on cheap rays
   const unsigned nfs = (unsigned)ta.fetch_shards;
+  // XCD-aware deal (32 shards; RT_XCD_CHUNK groups per chunk, 0: group g to shard g % 32):
+  // chunks of xc consecutive groups -- 64 by default, 4096 samples, ~41 pixels at 100 spp --
+  // go to the 4 shards of one XCD in turn (blocks are dispatched to the 8 XCDs round robin, so
+  // block b runs on XCD b % 8 and starts on a shard of its own XCD), so each XCD's L2 holds
+  // the nodes of its own image patches instead of every XCD caching every patch
+  const unsigned xc = nfs == 32u ? (unsigned)ta.xcd_chunk : 0u;
   const unsigned n_groups = (nq + 63u) >> 6;
   // wave-uniform work queue: [q_next, q_end)
   int sk = 0;
@@ -1154,14 +1164,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         if (freem == 0ull) break;
         if (q_next >= q_end) {  // next 64 slots: this shard's counter, then the other shards'
           for (;;) {
-            const int sh = (int)((blockIdx.x + sk) % nfs);
+            int sh;
+            if (xc > 0u) {  // this block's XCD's shards first, then the other XCDs'
+              const unsigned xo = (unsigned)sk / 4u, po = (unsigned)sk % 4u;
+              sh = (int)(((blockIdx.x % 8u + xo) % 8u) + 8u * ((blockIdx.x / 8u + po) % 4u));
+            } else {
+              sh = (int)((blockIdx.x + sk) % nfs);
+            }
             unsigned j = 0;
-            if ((unsigned)sh < n_groups) {
+            if (xc > 0u || (unsigned)sh < n_groups) {
               if (lane == 0) j = atomicAdd(ta.fetch + sh * kFetchStride, 1u);
               j = __shfl(j, 0);
             }
-            const unsigned g = (unsigned)sh + j * nfs;
-            if ((unsigned)sh < n_groups && g < n_groups) {
+            unsigned g;
+            if (xc > 0u) {  // shard sh = XCD x + 8 p: the chunks k of XCD x (chunk % 8 == x), offsets == p (mod 4)
+              const unsigned per = xc / 4u, k = j / per;
+              g = ((k * 8u + (unsigned)sh % 8u) * xc) + (unsigned)sh / 8u + (j % per) * 4u;
+            } else {
+              g = (unsigned)sh + j * nfs;
+            }
+            if ((xc > 0u || (unsigned)sh < n_groups) && g < n_groups) {
               q_next = (unsigned)ta.slot_base + g * 64u;
               q_end = (unsigned)ta.slot_base + min(g * 64u + 64u, nq);
               // 64-slot groups are slot-waves of the logic step: skip one whose slots retired
@@ -3051,6 +3073,8 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.hit_uv = s->d_hit_uv;
   ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   ta.fetch_shards = fetch_shards_env();
+  ta.xcd_chunk = RT_XCD_CHUNK_DEFAULT;
+  if (const char* e = std::getenv("RT_XCD_CHUNK")) ta.xcd_chunk = std::max(0, std::atoi(e)) & ~3;
   ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;

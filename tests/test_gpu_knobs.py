@@ -63,6 +63,9 @@ KNOBS = [
     {"RT_DRAIN_HELP": "0", **STEPS},  # the step pipeline without helpers
     {"RT_TRACE_SEVEN": "1"},  # the 7-wave planes instances (whole frames' default) on a small call
     {"RT_TRACE_SEVEN": "1", "RT_LDS_STACK": "3", **STEPS},  # ... through the step pipeline, deep stacks spilling
+    {"RT_XCD_CHUNK": "0"},  # the round-robin deal of the work queue (group g to shard g % 32)
+    {"RT_XCD_CHUNK": "4", **STEPS},  # the smallest XCD chunks, through the step pipeline
+    {"RT_XCD_CHUNK": "100000"},  # one chunk larger than the call: one XCD's shards, the rest stolen
     # step-pipeline knobs on a one-pass scene: ignored (one message each), still one-pass
     {"RT_FUSE": "1"},
     {"RT_FUSE": "0", "RT_SLOTS": "4096", "RT_PIPES": "2", "RT_DIAG": "1"},
