@@ -2919,12 +2919,13 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // 6263, 64M 6184, all 6319) or one rank's half of it (52M: 32M 5885, all 6225) -- else 128M
   // (C5 1.07G units: 96M 7666, 128M 7703, 192M 7705); scenes with reflection / refraction keep
   // 16M (C4: 8M 13043, 16M 13065, 32M 12791: their slots carry the Trace frames and take many
-  // short steps).  ~180 B of HBM per slot: 128M slots ~23 GB.
+  // short steps) -- since r05 6M in two slot pipelines (below).  ~180 B of HBM per slot: 128M
+  // slots ~23 GB.
   const bool frames_scene = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
   const bool tex_scene = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   const bool one_pass = one_pass_scene(s) && one_pass_env() && n_units <= one_pass_cap();
   if (one_pass) note_ignored_knobs();
-  long long slots = frames_scene ? std::min(n_units, 16LL << 20) : std::min(n_units, 128LL << 20);
+  long long slots = frames_scene ? std::min(n_units, 6LL << 20) : std::min(n_units, 128LL << 20);
   if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
   // slot-state words are addressed S[field * N + slot] in 32-bit int: (highest field + 1) * N
   // <= 2^31.  Scenes without Trace frames touch fields up to F_RAY + 2 (the ray origin), scenes
@@ -3165,8 +3166,11 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // (headline 4967 vs 5521 Mrays/s); with them the drain is short and one pipeline wins
   // everywhere (r03, one box, RT_PIPES=2 vs 1): headline 6050 / 6251, one rank's half / quarter /
   // eighth 5535 / 5875, 5239 / 5948, 4961 / 5357, C3 19955 / 20374, C4 12782 / 12979, C5 7492 /
-  // 7683 -- one by default, RT_PIPES=2..4 on request.
-  int n_pipes = n_units <= (4LL << 20) ? 1 : pipes_env();
+  // 7683 -- one by default, RT_PIPES=2..4 on request.  Scenes with Trace frames (reflection /
+  // refraction: many short steps, a logic step ~25 % of each) take two since r05, with 6M slots
+  // between them (C4, same box, 3 reps: one pipeline of 16M 13531-13563 Mrays/s, two of 6M
+  // 14135-14190, two of 8M 14044-14185, two of 12M 13691-13721, three of 12M 13886-13963).
+  int n_pipes = n_units <= (4LL << 20) ? 1 : frames_scene && !std::getenv("RT_PIPES") ? 2 : pipes_env();
   if (const char* e = std::getenv("RT_PIPES")) n_pipes = pipes_env();  // an explicit request holds for any size
   if (step_sync || one_pass) n_pipes = 1;
   n_pipes = std::max(1, std::min(n_pipes, n_slots / kBlock));  // every pipeline gets whole blocks of slots

@@ -7,7 +7,8 @@ units, costliest tiles first, their outputs remapped to the caller's order); C5 
 a rank's share of an 8-way split is rendered with two frames in flight, deferred, on two scene
 handles and streams.  Each test runs bench.py itself (`--dump-frame`: after the timed steps the
 frame at --seed is rendered by the same calls -- same frames in flight, issued behind another
-frame still in flight -- and saved) and compares it with the oracle (counter RNG) bit for bit:
+frame still in flight -- and saved) and compares it with the oracle (counter RNG) bit for bit
+(r05: the C3 and C4 frames as timed too -- C4 on the step pipeline's two slot pipelines):
 the whole headline frame and the whole rank share, with equal ray counts (the timed frame with
 --steps 1 is the frame at --seed: config.rays_per_step); for C5 a spread of tiles (the whole
 frame is ~1.5G rays, hours for the CPU restatement), so its ray count is not compared.
@@ -101,6 +102,51 @@ def test_c5_frame_as_timed(tmp_path_factory, tmp_path, gpu):
     tiles = [32 * 64 + 32, 0, 63, 63 * 64, 63 * 64 + 63, 32 * 64 + 11, 32 * 64 + 52, 11 * 64 + 32, 52 * 64 + 20,
              44 * 64 + 47]
     _compare(img, path, 4096, 8, tiles)
+
+
+def _scene_as_bench_writes(tmp_path, name, light_radius=None):
+    """The scene file bench.py renders for --scene NAME (--light-radius): resolution 1024^2 and
+    the light radius set, as bench.py writes it (bench.py:389-401)."""
+    src = os.path.join(ROOT, "tests", "golden", "scenes", "blend", name + ".json")
+    sc = json.load(open(src))
+    sc["render"] = {"resolution_x": 1024, "resolution_y": 1024}
+    if light_radius is not None:
+        for light in sc.get("lights", []):
+            light["radius"] = light_radius
+    p = str(tmp_path / (name + "_bench.json"))
+    with open(p, "w") as f:
+        json.dump(sc, f)
+    return src, p
+
+
+def test_c3_frame_as_timed(tmp_path, gpu):
+    """C3 as timed: the whole Antialiasing frame (1024^2 x 100 spp) in one one-pass call over all
+    256 tiles (transformed shapes: byte-code nodes, fused point-light shadows in the tracing
+    lane); the cube's faces and silhouette and the lit floor against the oracle."""
+    src, path = _scene_as_bench_writes(tmp_path, "Antialiasing")
+    img, line = _bench(tmp_path, "c3", "--scene", src)
+    assert line["config"]["pipeline"].startswith("one-pass") and line["config"]["frames_in_flight"] == 1
+    assert np.isfinite(img).all()
+    _compare(img, path, 1024, 10, [9 * 16 + 7, 12 * 16 + 6, 7 * 16 + 6, 3 * 16 + 12, 0, 255])
+
+
+def test_c4_frame_as_timed(tmp_path, gpu):
+    """C4 as timed: the whole glossy_reflection frame (light radius 1.0, -light_sample 4) on the
+    step pipeline with its defaults for scenes with Trace frames -- two slot pipelines on two
+    streams, 6M slots between them, ~40 steps; tiles over the spheres, the cube and their
+    reflections against the oracle."""
+    src, path = _scene_as_bench_writes(tmp_path, "glossy_reflection", light_radius=1.0)
+    img, line = _bench(tmp_path, "c4", "--scene", src, "--light-radius", "1.0", "--light-samples", "4")
+    assert line["config"]["pipeline"].startswith("steps")
+    assert np.isfinite(img).all()
+    tiles_x = 16
+    regions = [((t % tiles_x) * T, (t // tiles_x) * T, T, T) for t in [14 * 16 + 7, 10 * 16 + 4, 11 * 16 + 12, 7 * 16 + 9]]
+    ref, _ = ob.render_regions(path, regions, use_bvh=True, spp_sqrt=10, light_samples=4, seed=SEED,
+                               resolution=(1024, 1024))
+    for k, (x0, y0, _, _) in enumerate(regions):
+        got = np.ascontiguousarray(img[y0:y0 + T, x0:x0 + T])
+        bad = int((got.view(np.uint32) != ref[k].view(np.uint32)).sum())
+        assert bad == 0, f"region {regions[k]}: {bad} channels differ from the oracle"
 
 
 def test_step_pipeline_scene_frames_in_flight(tmp_path, gpu):
