@@ -81,7 +81,10 @@ typedef struct rt_prim {
  *   meta byte k: 0 = no child (child[k] = -1, codes lo 255 / hi 0: an inverted box);
  *                0x01 = internal child (child[k] = node index);
  *                0x80 | n = leaf child with n primitives starting at f:
- *                child[k] = 0x80000000 | f << 7 | n  (f < 2^24, n < 128). */
+ *                child[k] = 0x80000000 | f << 7 | n  (f < 2^24, n < 128).
+ * rt_scene_create keeps its device copy in this layout for scenes with transformed shapes and
+ * re-packs it for planes-only scenes (80-B device nodes, the codes as fp16 integers for the
+ * kernel's mixed-precision fmas: the same values); the caller's array is not modified. */
 typedef struct rt_node4 {
   float origin[3];
   uint32_t exps;
