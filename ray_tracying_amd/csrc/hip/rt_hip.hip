@@ -1418,9 +1418,12 @@ __device__ __forceinline__ V3 diffuse_color(const LogicArgs& a, const rt_materia
 // blocks of 4 waves per CU = waves per SIMD).  The logic step is bound by the latency of its
 // scattered state loads, so occupancy pays: without frames 4 waves (<= 128 VGPRs; the
 // unconstrained allocation took 132 = 3 waves, 10 % slower frame); with recursion frames
-// the state machine needs ~195 (2 waves).  A/B builds: make variant VDEFS=-DRT_LOGIC_WAVES=5
+// the state machine needs ~195 (2 waves).  A/B builds: make variant VDEFS=-DRT_LOGIC_WAVES=6
+// r05, two slot pipelines: 5 waves for the reflection-frames instance (95-96 VGPRs, 4-6
+// spilled; the frameless instances fit 5 at 87-89 either way) -- C4 +2.0 % (same box, 2 reps:
+// 14296-14303 -> 14561-14597 Mrays/s; 6 waves spill 34-41)
 #ifndef RT_LOGIC_WAVES
-#define RT_LOGIC_WAVES 4
+#define RT_LOGIC_WAVES 5
 #endif
 #ifndef RT_LOGIC_WAVES_F
 #define RT_LOGIC_WAVES_F 2
