@@ -2436,7 +2436,7 @@ extern "C" {
 const char* rt_last_error(void) { return g_err.c_str(); }
 
 const char* rt_build_info(void) {
-  return "librt_hip: gfx950 hand-written HIP; wavefront logic+trace kernels; SAH BVH4 (64-B quantised nodes) + LDS stack; no MFMA";
+  return "librt_hip: gfx950 hand-written HIP; wavefront logic+trace kernels; SAH BVH4 (quantised nodes: fp16 codes for planes-only scenes, 8-bit otherwise) + LDS stack; one-pass and step pipelines; no MFMA";
 }
 
 int rt_device_count(int32_t* count) {
