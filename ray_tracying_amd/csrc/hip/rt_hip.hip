@@ -2539,6 +2539,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     return fail(RT_EINVAL, "rt_scene_create: inconsistent primitive/node arrays (at most 2^24 - 1 primitives)");
   if (d->n_nodes < 0 || d->n_nodes >= (1 << 26))
     return fail(RT_EINVAL, "rt_scene_create: at most 2^26 - 1 BVH4 nodes");
+  if (d->prim_stride == 64 && (int64_t)d->n_nodes * 80 > (int64_t)UINT32_MAX)  // 80-B device nodes at 32-bit byte offsets
+    return fail(RT_EINVAL, "rt_scene_create: at most 53687091 BVH4 nodes in a planes-only scene");
   if (d->stack_bound < 1 || d->stack_bound > 4096) return fail(RT_EINVAL, "rt_scene_create: stack_bound out of range");
   if (d->prim_stride != 64 && d->prim_stride != 128)
     return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
@@ -3089,7 +3091,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   ta.fetch_shards = fetch_shards_env();
   ta.xcd_chunk = RT_XCD_CHUNK_DEFAULT;
-  if (const char* e = std::getenv("RT_XCD_CHUNK")) ta.xcd_chunk = std::max(0, std::atoi(e)) & ~3;
+  if (const char* e = std::getenv("RT_XCD_CHUNK")) ta.xcd_chunk = std::min(std::max(0, std::atoi(e)), 1 << 20) & ~3;  // 32-bit group indices
   ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
