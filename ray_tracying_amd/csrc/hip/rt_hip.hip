@@ -761,7 +761,8 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 //
 // Per axis the ray's direction sign picks which of the two code words holds the near planes
 // of all four children (inv > 0: lo, else hi; one v_perm_b32 with a per-ray byte selector,
-// operands swapped for the far word), so each child needs one max3 and one min3
+// operands swapped for the far word; two per side with the fp16 codes of kF16, two planes
+// per word), so each child needs one max3 and one min3
 // instead of three min/max pairs.  Empty children carry inverted boxes (lo 255, hi 0) and
 // always miss; child entries come precomputed from the host (node index, or the encoded
 // leaf), so nothing is decoded here.  `lim` is the cull bound (cull_limit) of the query.
