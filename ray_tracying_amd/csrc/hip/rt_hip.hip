@@ -1175,9 +1175,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
         if (q_next >= q_end) {  // next 64 slots: this shard's counter, then the other shards'
           for (;;) {
             int sh;
-            if (xc > 0u) {  // this block's XCD's shards first, then the other XCDs'
+            // 7-wave instances: the deal's derived values recomputed here, in the cold fetch path,
+            // from opaque copies -- hoisted to the kernel's entry they stayed live across the
+            // whole loop (SGPRs spilled 111 -> 101; r05 A/B, 3 reps: headline +0.5 %, C5 +0.6 %;
+            // in the 6-wave instances one rank's eighth lost 0.8 %, so they keep the hoisting)
+            unsigned xcv = xc, bid = blockIdx.x;
+            if constexpr (kSeven) {
+              asm volatile("s_mov_b32 %0, %1" : "=s"(xcv) : "s"(xc));
+              asm volatile("s_mov_b32 %0, %1" : "=s"(bid) : "s"((unsigned)blockIdx.x));
+            }
+            if (xcv > 0u) {  // this block's XCD's shards first, then the other XCDs'
               const unsigned xo = (unsigned)sk / 4u, po = (unsigned)sk % 4u;
-              sh = (int)(((blockIdx.x % 8u + xo) % 8u) + 8u * ((blockIdx.x / 8u + po) % 4u));
+              sh = (int)(((bid % 8u + xo) % 8u) + 8u * ((bid / 8u + po) % 4u));
             } else {
               sh = (int)((blockIdx.x + sk) % nfs);
             }
@@ -1187,9 +1196,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
               j = __shfl(j, 0);
             }
             unsigned g;
-            if (xc > 0u) {  // shard sh = XCD x + 8 p: the chunks k of XCD x (chunk % 8 == x), offsets == p (mod 4)
-              const unsigned per = xc / 4u, k = j / per;
-              g = ((k * 8u + (unsigned)sh % 8u) * xc) + (unsigned)sh / 8u + (j % per) * 4u;
+            if (xcv > 0u) {  // shard sh = XCD x + 8 p: the chunks k of XCD x (chunk % 8 == x), offsets == p (mod 4)
+              const unsigned per = xcv / 4u, k = j / per;
+              g = ((k * 8u + (unsigned)sh % 8u) * xcv) + (unsigned)sh / 8u + (j % per) * 4u;
             } else {
               g = (unsigned)sh + j * nfs;
             }
