@@ -50,9 +50,15 @@ constexpr int kBlock = 256;
 // that run 6 waves/SIMD (6 blocks x 24 KB of LDS per CU), 11 for the 7-wave ones (7 x 22 KB),
 // 16 for the one at 5 (fused point-light shadows over transformed shapes: its hit-record code
 // needs the registers)
+// the production traversal instances (kFixed) take the three loop parameters as constants
+// -- the defaults, the LDS stack per waves/SIMD -- so they hold no SGPRs of their own;
+// render_tiles launches them when a call's values are exactly these, else the runtime-knob
+// instances (RT_REFILL, RT_LEAF_MIN, RT_LDS_STACK, a tree shallower than the stack)
+constexpr int kSevenStack = 11, kRefillDefault = 48, kLeafDefault = 24;
+constexpr int default_stack(int waves) { return waves >= 7 ? kSevenStack : waves == 6 ? 12 : 16; }
 static int lds_stack_entries(int waves) {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_LDS_STACK");
-  return e ? std::max(1, std::min(64, std::atoi(e))) : waves >= 7 ? 11 : waves == 6 ? 12 : 16;
+  return e ? std::max(1, std::min(64, std::atoi(e))) : default_stack(waves);
 }
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
@@ -961,7 +967,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 static int instance_waves(bool planes, bool fuse, bool soft, bool seven) {
   return seven ? 7 : (fuse && !planes) ? RT_TRACE_WAVES : (soft && !planes) ? RT_TRACE_WAVES_SOFT : RT_TRACE_WAVES_PLAIN;
 }
-template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft, bool kSeven = false>
+template <bool kCount, bool kPlanesOnly, bool kFuse, bool kSoft, bool kSeven = false, bool kFixed = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven), 8))) void trace_refill_kernel(TraceArgs ta) {
   extern __shared__ __attribute__((aligned(16))) int lds_stack[];
   const unsigned int nq = (unsigned)ta.n_work;
@@ -977,9 +983,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   // load, a field spilled to a VGPR lane is restored with its whole 8-dword tuple (8
   // v_readlane per use at the loop head; r04 A/B: headline +5 %, one rank's eighth +4 %, C5 +6 %)
   TraceArgs la = ta;
-  la.refill_min = sgpr_copy(ta.refill_min);
-  la.leaf_min = sgpr_copy(ta.leaf_min);
-  la.lds_entries = sgpr_copy(ta.lds_entries);
+  if constexpr (kFixed || kSeven) {  // constants (render_tiles checks the call's values): three
+    // SGPRs fewer live across the loop, whose spills were reloaded by a v_readlane each per
+    // iteration (r05 A/B, 7 waves: headline +4.6 %, C5 +5.2 %)
+    la.refill_min = kRefillDefault;
+    la.leaf_min = kLeafDefault;
+    la.lds_entries = default_stack(RT_INSTANCE_WAVES(kPlanesOnly, kFuse, kSeven));
+  } else {
+    la.refill_min = sgpr_copy(ta.refill_min);
+    la.leaf_min = sgpr_copy(ta.leaf_min);
+    la.lds_entries = sgpr_copy(ta.lds_entries);
+  }
   const TraceArgs& a = la;
   const unsigned int any = *ta.any_query;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ta.host_flag = any;  // read by the host after the step
@@ -2181,34 +2195,37 @@ void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_
   else hipLaunchKernelGGL((logic_kernel<F, R, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
 }
 // trace launch (the refill kernel; count: the instrumented variant)
-template <bool kCount>
-void launch_trace2(const TraceArgs& ta, bool planes, bool soft, bool seven, unsigned blocks, size_t lds, hipStream_t st) {
+template <bool kCount, bool kFixed>
+void launch_trace3(const TraceArgs& ta, bool planes, bool soft, bool seven, unsigned blocks, size_t lds, hipStream_t st) {
   if (!kCount && seven && planes && ta.n_fuse > 0)  // 7 waves/SIMD (whole frames; render_tiles)
-    hipLaunchKernelGGL((trace_refill_kernel<false, true, true, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<false, true, true, false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (!kCount && seven && planes && !soft)
-    hipLaunchKernelGGL((trace_refill_kernel<false, true, false, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<false, true, false, false, true, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (ta.n_fuse > 0 && planes)  // point lights only (the host's choice)
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, true, false, false, kFixed>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (ta.n_fuse > 0 || (ta.one_pass && !planes))  // ... and no textures: the fused path stores no (u, v);
                                                        // one-pass calls of transformed shapes: the lane computes
                                                        // the hit record (planes-only one-pass calls without
                                                        // lights take the plain planes instance below, whose
                                                        // finish_query writes a textured hit's (u, v))
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, true, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, true, false, false, kFixed>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (soft && planes)
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, true, false, kFixed>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (soft)
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, true>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, true, false, kFixed>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else if (planes)
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, true, false, false, false, kFixed>), dim3(blocks), dim3(kBlock), lds, st, ta);
   else
-    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, false>), dim3(blocks), dim3(kBlock), lds, st, ta);
+    hipLaunchKernelGGL((trace_refill_kernel<kCount, false, false, false, false, kFixed>), dim3(blocks), dim3(kBlock), lds, st, ta);
 }
 // trace launch: soft = the lanes continue soft-light shadow samples themselves (kSoft)
-void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, bool seven, unsigned blocks, size_t lds,
-                  hipStream_t st) {
-  if (count) launch_trace2<true>(ta, planes, soft, seven, blocks, lds, st);
-  else launch_trace2<false>(ta, planes, soft, seven, blocks, lds, st);
+// fixed: the call's loop parameters are the instance's defaults (kFixed instances; not for
+// the instrumented count_work launches, which keep runtime values)
+void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, bool seven, bool fixed, unsigned blocks,
+                  size_t lds, hipStream_t st) {
+  if (count) launch_trace3<true, false>(ta, planes, soft, seven, blocks, lds, st);
+  else if (fixed) launch_trace3<false, true>(ta, planes, soft, seven, blocks, lds, st);
+  else launch_trace3<false, false>(ta, planes, soft, seven, blocks, lds, st);
 }
 static int pipes_env() {  // read per call: tests vary it within one process
   const char* e = std::getenv("RT_PIPES");
@@ -2232,14 +2249,14 @@ static int batch_shards_env() {
 static int leaf_min_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_LEAF_MIN");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : 24;  // r03 sweep at 32M slots: 12 / 16 / 24 / 32 (two pipelines)
+    return e ? std::max(1, std::min(64, std::atoi(e))) : kLeafDefault;  // r03 sweep at 32M slots: 12 / 16 / 24 / 32 (two pipelines)
   }();
   return v;
 }
 static int refill_min_env() {
   static const int v = [] {
     const char* e = std::getenv("RT_REFILL");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : 48;
+    return e ? std::max(1, std::min(64, std::atoi(e))) : kRefillDefault;
   }();
   return v;
 }
@@ -2656,8 +2673,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
                                                    : (const void*)trace_refill_kernel<false, false, false, true>,
                                             instance_waves(planes, false, true, false));
     if (planes) {
-      s->trace_blocks_per_cu_seven = occupancy((const void*)trace_refill_kernel<false, true, false, false, true>, 7);
-      s->trace_blocks_per_cu_fuse_seven = occupancy((const void*)trace_refill_kernel<false, true, true, false, true>, 7);
+      s->trace_blocks_per_cu_seven = occupancy((const void*)trace_refill_kernel<false, true, false, false, true, true>, 7);
+      s->trace_blocks_per_cu_fuse_seven = occupancy((const void*)trace_refill_kernel<false, true, true, false, true, true>, 7);
     }
 
     s->n_cu = ncu;
@@ -3135,7 +3152,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.n_fuse = n_units <= 2LL * n_slots || s->desc.n_prims < kFuseFewPrims ? s->fuse_lights : 0;
   if (const char* e = std::getenv("RT_FUSE"))  // (a one-pass call traces every point light's shadow ray fused)
     if (!one_pass) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
-  // the launched instance (launch_trace2): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
+  // the launched instance (launch_trace3): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
   // entries except fused shadows over transformed shapes (5, 16)
   ta.one_pass = one_pass ? 1 : 0;
   ta.tile_cost = nullptr;
@@ -3167,8 +3184,15 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   bool seven = planes_only && !soft_launch && !p->count_work && p->sync != 0 && n_units > (32LL << 20);
   if (const char* e = std::getenv("RT_TRACE_SEVEN"))
     seven = planes_only && !soft_launch && !p->count_work && std::atoi(e) != 0;
+  // the 7-wave instances have the default loop parameters built in: another stack depth (a
+  // shallow tree, RT_LDS_STACK) or threshold (RT_REFILL, RT_LEAF_MIN) takes the 6-wave ones
+  if (seven && (std::min(s->desc.stack_bound, lds_stack_entries(7)) != kSevenStack || ta.refill_min != kRefillDefault ||
+                ta.leaf_min != kLeafDefault))
+    seven = false;
   const int trace_waves = instance_waves(planes_only, fuse_launch, soft_launch, seven);
   ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(trace_waves));
+  const bool fixed = ta.lds_entries == default_stack(trace_waves) && ta.refill_min == kRefillDefault &&
+                     ta.leaf_min == kLeafDefault;
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
   la.occl = s->d_occl;
@@ -3323,7 +3347,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
-    launch_trace(P.ta, p->count_work != 0, planes_only, false, seven, P.trace_blocks, lds, stream);
+    launch_trace(P.ta, p->count_work != 0, planes_only, false, seven, fixed, P.trace_blocks, lds, stream);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
     const unsigned rblocks = (unsigned)((n_pixels + kSrPixels - 1) / kSrPixels);
@@ -3381,7 +3405,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
-        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, seven, P.trace_blocks, lds, P.st);
+        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, seven, fixed, P.trace_blocks, lds, P.st);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
         HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
       }
