@@ -405,6 +405,15 @@ __device__ __forceinline__ void test_prims(const TraceArgs& a, int first, int cn
   }
 }
 
+// Lanes set in a wave-uniform mask, as a 32-bit SGPR value: with __popcll the compiler kept
+// the i64 popcount and compared it in 64 bits -- a VALU v_cmp_gt_u64 (gfx9 has no 64-bit
+// scalar ordered compare) at the loop head and the leaf check of every iteration
+__device__ __forceinline__ int popc_s(uint64_t m) {
+  int c;
+  asm("s_bcnt1_i32_b64 %0, %1" : "=s"(c) : "s"(m));
+  return c;
+}
+
 // a wave-uniform value in an SGPR of its own (opaque to the optimiser: not re-fused with the
 // wide load it came from)
 __device__ __forceinline__ int sgpr_copy(int v) {
@@ -1181,7 +1190,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   for (;;) {
     RT_PT_MARK(3);  // loop control (ballots) since the node phase
     uint64_t act = __ballot(item != kNoItem);
-    if (__popcll(act) < a.refill_min) {
+    if (popc_s(act) < a.refill_min) {
       if (slot >= 0 && item == kNoItem) settle();
       while (!exhausted) {
         const uint64_t freem = __ballot(slot < 0);
@@ -1259,7 +1268,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     }
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
     const uint64_t leafm = __ballot(is_leaf_item(item));
-    if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+    if (leafm != 0ull && (popc_s(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
 #ifdef RT_PHASE_TIMING
       {
         const int c = is_leaf_item(item) ? (int)((uint32_t)item & 0x7fu) : 0;
@@ -1393,7 +1402,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       }
       const uint64_t act = __ballot(item != kNoItem);
       const uint64_t leafm = __ballot(is_leaf_item(item));
-      if (leafm != 0ull && (__popcll(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
+      if (leafm != 0ull && (popc_s(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
         if (is_leaf_item(item)) {
           const uint32_t e = (uint32_t)item;
           test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par,
