@@ -804,7 +804,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
     // rank's eighth +2.3 %, C5 +3.6 %; the code pairs picked by a per-lane load address
     // instead of the perms: -13 %, eight loads per visit).  Transformed-shape instances keep the
     // byte codes: there the wider node cost 10 more spilled VGPRs (C3 -4.5 %).
-    const char* nb = reinterpret_cast<const char*>(a.c.nodes) + ((uint32_t)node << 4);  // entry = node index x 5
+    const char* nb = reinterpret_cast<const char*>(a.c.nodes) + (uint32_t)node;  // entry = the node's byte offset
     const float4 g = *reinterpret_cast<const float4*>(nb);
     const int4 qc = *reinterpret_cast<const int4*>(nb + 64);
     uint32_t nx0, nx1, fx0, fx1, ny0, ny1, fy0, fy1, nz0, nz1, fz0, fz1;
@@ -2501,7 +2501,8 @@ static int upload(void** dst, const void* src, size_t bytes) {
 // transformed shapes keep the 64-B rt_node4 records; planes-only scenes get 80-B device nodes
 // -- origin + exponents (valid-child mask in the top byte), per axis the words (lo01, lo23,
 // hi01, hi23) of fp16 plane codes (exact: codes < 256), the child entries with internal
-// children as node index x 5 (the node's byte offset / 16) -- for node_visit's mixed fmas
+// children as the node's byte offset (node index x 80: no shift per visit) -- for
+// node_visit's mixed fmas
 struct NodeF16 {
   float origin[3];
   uint32_t exps;
@@ -2524,7 +2525,7 @@ static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n, bool plane
     for (int k = 0; k < 4; ++k) {
       const uint32_t m = (s.meta >> (8 * k)) & 0xffu;
       if (m) valid |= 1u << k;
-      d.child[k] = m == 0x01u ? s.child[k] * 5 : s.child[k];
+      d.child[k] = m == 0x01u ? s.child[k] * 80 : s.child[k];  // < 2^31 (rt_scene_create)
     }
     for (int a = 0; a < 3; ++a) d.origin[a] = s.origin[a];
     d.exps = (s.exps & 0xffffffu) | valid << 24;
@@ -2575,8 +2576,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     return fail(RT_EINVAL, "rt_scene_create: inconsistent primitive/node arrays (at most 2^24 - 1 primitives)");
   if (d->n_nodes < 0 || d->n_nodes >= (1 << 26))
     return fail(RT_EINVAL, "rt_scene_create: at most 2^26 - 1 BVH4 nodes");
-  if (d->prim_stride == 64 && (int64_t)d->n_nodes * 80 > (int64_t)UINT32_MAX)  // 80-B device nodes at 32-bit byte offsets
-    return fail(RT_EINVAL, "rt_scene_create: at most 53687091 BVH4 nodes in a planes-only scene");
+  if (d->prim_stride == 64 && (int64_t)d->n_nodes * 80 > (int64_t)INT32_MAX)  // 80-B device nodes, entries = byte offsets
+    return fail(RT_EINVAL, "rt_scene_create: at most 26843545 BVH4 nodes in a planes-only scene");
   if (d->stack_bound < 1 || d->stack_bound > 4096) return fail(RT_EINVAL, "rt_scene_create: stack_bound out of range");
   if (d->prim_stride != 64 && d->prim_stride != 128)
     return fail(RT_EINVAL, "rt_scene_create: prim_stride must be 64 or 128");
