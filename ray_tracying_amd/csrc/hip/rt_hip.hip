@@ -60,6 +60,14 @@ static int lds_stack_entries(int waves) {  // read per call: tests vary it withi
   const char* e = std::getenv("RT_LDS_STACK");
   return e ? std::max(1, std::min(64, std::atoi(e))) : default_stack(waves);
 }
+// LDS stack entries of a launch: the instance's default rows even for a tree shallower than
+// them (the rows past its depth stay unused; the kFixed instances assume the default), an
+// RT_LDS_STACK request -- and the soft-light chain instances, which keep runtime values and
+// whose 16 default rows at 5 waves/SIMD would fill a CU's LDS (C4 -0.9 %) -- capped at the
+// tree's depth bound
+static int call_lds_entries(int stack_bound, int waves, bool soft) {
+  return std::getenv("RT_LDS_STACK") || soft ? std::min(stack_bound, lds_stack_entries(waves)) : default_stack(waves);
+}
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
 constexpr int kCtlBytes = 4096;    // control block (cleared by init_kernel)
@@ -2665,8 +2673,8 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
     int ncu = 0, bpc = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 256;
     const bool planes = d->prim_stride == 64;
-    auto occupancy = [&](const void* fn, int waves) {
-      const int lds_entries = std::min(d->stack_bound, lds_stack_entries(waves));
+    auto occupancy = [&](const void* fn, int waves, bool soft = false) {
+      const int lds_entries = call_lds_entries(d->stack_bound, waves, soft);
       const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
       int b = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, lds_bytes) != hipSuccess || b < 1) b = 2;
@@ -2681,7 +2689,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
                                             instance_waves(planes, true, false, false));
     s->trace_blocks_per_cu_soft = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, true>
                                                    : (const void*)trace_refill_kernel<false, false, false, true>,
-                                            instance_waves(planes, false, true, false));
+                                            instance_waves(planes, false, true, false), true);
     if (planes) {
       s->trace_blocks_per_cu_seven = occupancy((const void*)trace_refill_kernel<false, true, false, false, true, true>, 7);
       s->trace_blocks_per_cu_fuse_seven = occupancy((const void*)trace_refill_kernel<false, true, true, false, true, true>, 7);
@@ -3132,7 +3140,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
-  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(6));  // set again below (instance)
+  ta.lds_entries = call_lds_entries(s->desc.stack_bound, 6, false);  // set again below (instance)
   // the refill kernel's leaf items hold first << 7 in 31 bits
   ta.refill_min = refill_min_env();
   ta.leaf_min = leaf_min_env();
@@ -3196,12 +3204,14 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     seven = planes_only && !soft_launch && !p->count_work && std::atoi(e) != 0;
   // the 7-wave instances have the default loop parameters built in: another stack depth (a
   // shallow tree, RT_LDS_STACK) or threshold (RT_REFILL, RT_LEAF_MIN) takes the 6-wave ones
-  if (seven && (std::min(s->desc.stack_bound, lds_stack_entries(7)) != kSevenStack || ta.refill_min != kRefillDefault ||
+  if (seven && (call_lds_entries(s->desc.stack_bound, 7, false) != kSevenStack || ta.refill_min != kRefillDefault ||
                 ta.leaf_min != kLeafDefault))
     seven = false;
   const int trace_waves = instance_waves(planes_only, fuse_launch, soft_launch, seven);
-  ta.lds_entries = std::min(s->desc.stack_bound, lds_stack_entries(trace_waves));
-  const bool fixed = ta.lds_entries == default_stack(trace_waves) && ta.refill_min == kRefillDefault &&
+  ta.lds_entries = call_lds_entries(s->desc.stack_bound, trace_waves, soft_launch);
+  // (soft-light chain launches keep the runtime-knob instance: their kFixed build spilled more
+  // SGPRs, C4 -0.8 %)
+  const bool fixed = !soft_launch && ta.lds_entries == default_stack(trace_waves) && ta.refill_min == kRefillDefault &&
                      ta.leaf_min == kLeafDefault;
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
