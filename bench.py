@@ -27,7 +27,7 @@ time vs 8 TB/s, and `l2` = algorithmic bytes (80 B per BVH4 node visit in planes
 64 B otherwise, + the primitive record per primitive test, counted by an instrumented run of the same frame) / launch time vs the L2's 34.5 TB/s.
 Scenes of a few primitives (C1-C4) get no roofline claim.
 cpu_baseline: the compiled reference (oracle/_ref/ref_driver; kind "reference") -- or the
-oracle restatement if the reference binary is absent (kind "port") -- on rank 0 at N=1,
+oracle restatement if the reference binary is absent (kind "port") -- on rank 0 at every N, after timing,
 single-threaded, on a bounded sample of the same frame (12 rows spread evenly over it; its
 rays/sample beside the frame's); plus the same number of rows run as 16 concurrent
 single-threaded processes (the job's CPU share on the GPU box).
@@ -66,6 +66,28 @@ def valu_peak(path):
         if d.get("max_valu_wave_instr_per_cu_cycle"):
             return float(d["max_valu_wave_instr_per_cu_cycle"]), f"{os.path.relpath(path, ROOT)} ({d.get('label', '')})"
     return 1.0, "assumed 1 wave64 instruction per CU-cycle (no counter-measured microbenchmark found)"
+def valu_block(pv: dict, pmc_valu: str, peak_ipc: float, peak_src: str) -> dict:
+    """The traversal kernel's VALU roofline from a pmc_valu.py summary: useful lane-ops/s (PMC wave64
+    VALU instructions/s x 64 x lane utilisation) against the guide's peak (`frac`, VERDICT r05 item
+    6), and against the highest issue rate measured on this chip (`frac_vs_measured`)."""
+    peak_tops = N_CU * peak_ipc * 64 * MAX_CLOCK_GHZ / 1e3
+    spec_tops = N_CU * SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3
+    achieved = pv["valu_g_wave_instr_per_s"] * 64 * pv["lane_utilisation"] / 1e3
+    return {"achieved": round(achieved, 3), "frac": round(achieved / spec_tops, 4),
+            "frac_vs_spec": round(achieved / spec_tops, 4), "spec_peak": round(spec_tops, 2),
+            "frac_vs_measured": round(achieved / peak_tops, 4), "measured_peak": round(peak_tops, 2),
+            "measured_peak_source": peak_src,
+            "issue_frac": round(pv["valu_g_wave_instr_per_s"] / (N_CU * peak_ipc * MAX_CLOCK_GHZ), 4),
+            "lane_utilisation": pv["lane_utilisation"], "measured_clock_ghz": pv.get("clock_ghz"),
+            "source": f"{os.path.relpath(pmc_valu, ROOT)} ({pv.get('label', '')})"}
+
+
+def cpu_baseline_rank(args) -> int | None:
+    """The rank that times the reference CPU path after the timed steps: rank 0 at every N (the
+    north_star asks for it beside the 1, 2, 4 and 8-GPU numbers), none with --no-cpu-baseline."""
+    return None if args.no_cpu_baseline else 0
+
+
 # one BVH4 node per visit: 80 B in planes-only scenes (fp16 plane codes), 64 B otherwise;
 # one 64-B plane / 128-B transformed record per primitive test
 NODE_BYTES_PLANES, NODE_BYTES_OTHER = 80, 64
@@ -247,6 +269,10 @@ def parse():
                          "when this rank renders at most 4M samples per frame (C2), 2 up to 32M (a rank's share of a 4- "
                          "or 8-way split), else 1 (whole frames lose: their traversals interleave instead of overlapping "
                          "at the tail)")
+    ap.add_argument("--frames-per-call", type=int, default=0,
+                    help="frames rendered by one rt_render_frames call (one camera pass, one traversal launch, one "
+                         "shading pass for all of them; one-pass scenes): 0 (auto) = the split N for a rank's share "
+                         "of an N-way split (so each call has the whole frame's samples), else 1")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render the frame at --seed with the timed steps' calls (same frames in "
                          "flight), gather it and save it (rank 0) as an (H, W, 3) .npy; unrendered tiles NaN")
@@ -366,7 +392,14 @@ def main():
         # the per-rank summary's collective with stand-in timings (rank r: r + 1 ms of render per step)
         summ = rank_summary(dist, "cpu", world, 1, 0.001 * (rank + 2), 1.0 * (rank + 1), 0.5, 1000.0 * (rank + 1))
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_in_group": ranks_in_group, "ranks": summ}),
+            # what the rendered line would carry besides: the rank timing the CPU baseline, and the
+            # VALU roofline block from the committed headline PMC summary
+            pv_path = os.path.join(ROOT, "profiles", PMC_PROFILE + "_pmc_valu.json")
+            pv = json.load(open(pv_path)) if os.path.exists(pv_path) else None
+            peak_ipc, peak_src = valu_peak(os.path.join(ROOT, "profiles", UBENCH_PROFILE + "_ubench_valu_pmc.json"))
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_in_group": ranks_in_group, "ranks": summ,
+                              "cpu_baseline_rank": cpu_baseline_rank(args),
+                              "roofline_valu": valu_block(pv, pv_path, peak_ipc, peak_src) if pv else None}),
                   flush=True)
         if dist:
             dist.destroy_process_group()
@@ -496,15 +529,60 @@ def main():
     # rays and this frame's shading run in the idle tail of the other frame's trace launch.
     # Every frame is rendered in full and gathered; steps are timed exactly as with F = 1.
     units = len(mine) * T * T * max(1, args.spp_sqrt) ** 2
+    # Frames per call (r06): a rank's share of a split frame renders B consecutive frames in ONE
+    # rt_render_frames call -- every sample of them in one camera pass, one traversal launch and
+    # one shading pass -- so its launches have the whole frame's size (B = the split: 8 frames of
+    # an eighth = 105M samples) and run what a whole frame runs (the 7-wave traversal, one short
+    # tail per B frames) instead of a launch an eighth that size, whose drain and missing seventh
+    # wave held one rank's eighth at 0.84 of the whole frame's rate (r05).  Every
+    # frame is still rendered in full (its own seed) and gathered; the timed steps are the same K
+    # frames.  Step-pipeline scenes render one frame per call.
+    one_pass_path = cst.path == rt.PATH_ONE_PASS
+    B = args.frames_per_call if args.frames_per_call > 0 else (
+        max(1, min(split, (2 ** 30) // max(units, 1))) if one_pass_path and split > 1 else 1)
+    if not one_pass_path:
+        B = 1
+    if B > 1:
+        out = torch.zeros(B * out.numel(), dtype=torch.float32, device=f"cuda:{dev}")
+    share_floats = out.numel() // B  # per frame, padded to the largest rank's share (equal gathers)
     # auto (one box, r04): C2's 1.05M samples 2,606 / 2,786 / 2,690 Mrays/s at F = 2 / 3 / 4; one
     # rank's eighth (18M) 6,322 at F = 2, 5,926 at F = 3; whole frames keep one.  Step-pipeline
     # calls (reflection, refraction, soft lights) complete before returning: nothing to overlap
-    # (ADVICE r04), so they keep one frame in flight
+    # (ADVICE r04), so they keep one frame in flight; multi-frame calls are whole-frame sized
     F = args.frames_in_flight if args.frames_in_flight > 0 else (
-        1 if cst.path != rt.PATH_ONE_PASS else 3 if units <= 4 * 2 ** 20 else 2 if units <= 32 * 2 ** 20 else 1)
+        1 if not one_pass_path or B > 1 else 3 if units <= 4 * 2 ** 20 else 2 if units <= 32 * 2 ** 20 else 1)
+    if B > 1 and F > 1:
+        raise SystemExit("bench.py: --frames-per-call > 1 renders synchronous calls (--frames-in-flight 1)")
     fl_ds = [ds] + [rt.DeviceScene(scene, dev) for _ in range(F - 1)]
     fl_out = [out] + [torch.zeros_like(out) for _ in range(F - 1)]
     fl_st = [torch.cuda.Stream(device=dev) for _ in range(F)] if F > 1 else []
+    last_group = [1]  # frames in the last call's buffer (the last gathered frame is its last)
+
+    def groups(seeds):
+        """The frames split into calls of at most B, as evenly as possible (20 frames, B = 8:
+        7 + 7 + 6), so that no call is much smaller than the others."""
+        n = len(seeds)
+        if n == 0:
+            return []
+        k = -(-n // B)
+        sizes = [n // k + (1 if i < n % k else 0) for i in range(k)]
+        out_g, i = [], 0
+        for sz in sizes:
+            out_g.append(seeds[i:i + sz])
+            i += sz
+        return out_g
+
+    def multi(seeds):
+        """B > 1: each group of frames is one rt_render_frames call into `out` (frame-major), then
+        one gather of the group's frames."""
+        sts = []
+        for g in groups(seeds):
+            params.seed = g[0]
+            st = ds.render_frames(g, mine, T, T, out.data_ptr(), params)
+            last_group[0] = len(g)
+            gather(out[:len(g) * share_floats])
+            sts.append(st)
+        return sts
 
     def issue(k, seed):
         i = k % F
@@ -520,7 +598,10 @@ def main():
 
     def run_frames(seeds):
         """Render the frames (F in flight) and return their stats in order; the last frame's
-        buffer is fl_out[(len(seeds) - 1) % F] (gathered: `gathered`)."""
+        buffer is fl_out[(len(seeds) - 1) % F] (gathered: `gathered`).  With B > 1 frames per
+        call: one entry per call, and the last frame is the last of `out`'s last_group[0]."""
+        if B > 1:
+            return multi(seeds)
         if F == 1:
             return [step(sd) for sd in seeds]
         sts = []
@@ -571,22 +652,34 @@ def main():
     rays_all, trace_ms_all, launches_all, alg_bytes_all, busy_ms_all = tot.tolist()
     elapsed = tmax.item()
 
+    def last_frame(buf, r):
+        """The last frame of rank r's gathered / rendered buffer (B > 1: rt_render_frames wrote its
+        frames end to end, rank r's own tile count apart; the buffer is padded to the largest
+        share so that every rank gathers the same size)."""
+        a = buf.cpu().numpy()
+        if B > 1:
+            n = last_group[0]
+            own = len(tl.assign_tiles(n_tiles, split, r, tiles_x, deal)) * T * T * 3
+            a = a[:n * own].reshape(n, own)[-1]
+        return a
+
     if rank == 0 and dist:  # sanity: the gathered frame has every pixel, all finite
-        img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H, deal)
+        img = tl.unpack([last_frame(g, r) for r, g in enumerate(gathered)], world, n_tiles, T, W, H, deal)
         assert np.isfinite(img).all()
     if args.dump_frame:
         # The frame at --seed rendered by the calls the timed steps make (same F, handles and
-        # streams), issued last behind F - 1 other frames still in flight, gathered, saved by
-        # rank 0 as an (H, W, 3) float32 image; tiles no rank rendered (--emulate) are NaN.
-        run_frames([args.seed + 2000 + k for k in range(F - 1)] + [args.seed])
+        # streams), issued last behind F - 1 other frames still in flight -- or, with B frames per
+        # call, as the last frame of a call of B -- gathered, saved by rank 0 as an (H, W, 3)
+        # float32 image; tiles no rank rendered (--emulate) are NaN.
+        run_frames([args.seed + 2000 + k for k in range(max(F, B) - 1)] + [args.seed])
         torch.cuda.synchronize()
         if rank == 0:
             if dist:
-                img = tl.unpack([g.cpu().numpy() for g in gathered], world, n_tiles, T, W, H, deal)
+                img = tl.unpack([last_frame(g, r) for r, g in enumerate(gathered)], world, n_tiles, T, W, H, deal)
             else:
                 last = fl_out[F - 1] if F > 1 else out
                 img = np.full((H, W, 3), np.nan, dtype=np.float32)
-                buf = last.cpu().numpy().reshape(-1, T, T, 3)
+                buf = last_frame(last, args.emulate_rank if args.emulate > 1 else 0).reshape(-1, T, T, 3)
                 for k, tid in enumerate(mine):
                     x0, y0 = (tid % tiles_x) * T, (tid // tiles_x) * T
                     w, h = min(T, W - x0), min(T, H - y0)
@@ -629,7 +722,7 @@ def main():
         pv = json.load(open(pmc_valu))
     kernel = {
         "kernel": "trace_refill_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
-        "launches_per_step": int(launches_all / args.steps / world),
+        "launches_per_step": round(launches_all / args.steps / world, 3),
         "trace_busy_ms_per_step": round(busy_ms_step, 3),
         # with F > 1 frames in flight the frames' launches overlap: their busy times sum past the
         # step time, and no share of it is measured
@@ -644,29 +737,22 @@ def main():
         roofline = {"bound": None, "frac": None, "achieved": None, "peak": None, "unit": None, "traffic": None,
                     "note": "scene of a few primitives (on-die): no roofline claim (SURVEY.md 8(d))", **kernel}
     else:
-        valu = None
         peak_ipc, peak_src = valu_peak(args.ubench or os.path.join(ROOT, "profiles", UBENCH_PROFILE + "_ubench_valu_pmc.json"))
-        peak_tops = N_CU * peak_ipc * 64 * MAX_CLOCK_GHZ / 1e3
         spec_tops = N_CU * SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE * 64 * MAX_CLOCK_GHZ / 1e3
-        if pv:
-            # useful lane-ops/s = wave64 VALU instructions/s x 64 x lane utilisation
-            achieved = pv["valu_g_wave_instr_per_s"] * 64 * pv["lane_utilisation"] / 1e3
-            valu = {"achieved": round(achieved, 3), "frac": round(achieved / peak_tops, 4),
-                    "frac_vs_spec": round(achieved / spec_tops, 4), "spec_peak": round(spec_tops, 2),
-                    "issue_frac": round(pv["valu_g_wave_instr_per_s"] / (N_CU * peak_ipc * MAX_CLOCK_GHZ), 4),
-                    "lane_utilisation": pv["lane_utilisation"], "measured_clock_ghz": pv.get("clock_ghz"),
-                    "source": f"{os.path.relpath(pmc_valu, ROOT)} ({pv.get('label', '')})"}
+        valu = valu_block(pv, pmc_valu, peak_ipc, peak_src) if pv else None
         # PMC bytes per launch (a serialised --pmc run) x launches per frame over the busy time
         hbm_rate = (traffic * launches_all / world / args.steps / (busy_ms_step * 1e-3) / 1e9
                     if traffic and busy_ms_step > 0 else None)
         roofline = {
             "bound": "valu",
-            "achieved": valu["achieved"] if valu else None, "peak": round(peak_tops, 2),
+            "achieved": valu["achieved"] if valu else None, "peak": round(spec_tops, 2),
             "unit": "T VALU lane-ops/s", "frac": valu["frac"] if valu else None,
             "traffic": traffic, "traffic_unit": "HBM bytes per trace launch (PMC)", "traffic_source": traffic_src,
-            "peak_definition": f"256 CUs x {peak_ipc:.3f} wave64 VALU instructions per CU-cycle (counter-measured: "
-                               f"{peak_src}) x 64 lanes x 2.4 GHz; valu.frac_vs_spec uses the guide's 2 per CU-cycle; "
-                               "achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation",
+            "peak_definition": "the guide's VALU peak (MI355X_MICROARCH.md: a wave64 instruction issues over 2 "
+                               "cycles on each of 4 SIMD-32 per CU = 2 wave64 instructions per CU-cycle) x 256 CUs x "
+                               "64 lanes x 2.4 GHz; achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation; "
+                               f"valu.frac_vs_measured prices it against the highest rate measured on this chip, "
+                               f"{peak_ipc:.3f} per CU-cycle ({peak_src})",
             "valu": valu,
             "hbm": {"achieved_gbs": round(hbm_rate, 1) if hbm_rate else None, "peak_gbs": HBM_PEAK_GBS,
                     "frac": round(hbm_rate / HBM_PEAK_GBS, 4) if hbm_rate else None,
@@ -684,7 +770,7 @@ def main():
             **kernel,
         }
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
+    if cpu_baseline_rank(args) == rank:  # after timing, at every N (north_star: beside 1/2/4/8 GPUs)
         cpu = cpu_baseline(scene_path, args, rank, rays_all / args.steps / (W * H * max(1, args.spp_sqrt) ** 2))
     line = {
         "metric": METRIC,
@@ -706,6 +792,7 @@ def main():
             "rays_per_step": int(rays_all / args.steps), "tile": T, "parallelism": f"image tiles x{world}" + (f" ({args.deal} deal)" if split > 1 else ""),
             "rng": "counter (splitmix64 per pixel/sample)",
             "frames_in_flight": F,
+            "frames_per_call": B,
             "pipeline": ("one-pass (camera_kernel -> one trace_refill_kernel launch -> shade_reduce_kernel)" if one_pass
                          else "steps (logic -> start -> trace over slot state, then reduce)"),
             **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),

@@ -112,7 +112,7 @@ typedef struct rt_material {
   float k_specular, shininess, roughness, reflectivity;
   float transparency, refractive_index;
   int32_t texture; /* index into rt_scene_desc.textures or -1 */
-  int32_t pad;
+  int32_t pad;     /* ignored: rt_scene_create derives its device copy's flags here */
 } rt_material;
 
 /* Point light (light.hpp:5-13), 32 bytes. */
@@ -221,6 +221,20 @@ int rt_scene_destroy(rt_scene_t scene);
 int rt_render_tiles(rt_scene_t scene, const rt_camera_desc* cam, const rt_render_params* params,
                     const int32_t* tile_ids, int32_t n_tiles, int32_t tile_w, int32_t tile_h,
                     float* d_rgb_out, void* stream, rt_stats* stats);
+
+/* Renders n_frames frames (1..1024) of the same tiles, frame f with counter-RNG seed seeds[f]
+ * (params->seed is not used), into d_rgb_out: frame f's n_tiles tiles at
+ * [f*n_tiles*tile_w*tile_h*3, (f+1)*n_tiles*tile_w*tile_h*3), each laid out as rt_render_tiles
+ * lays out its tiles.  Frame f equals rt_render_tiles with params->seed = seeds[f] bit for bit.
+ * One-pass scenes (rt_stats.path) render as many frames per pass as 2^30 samples hold -- every
+ * sample of them in one camera pass, one traversal launch and one shading pass -- so a small
+ * tile list (one rank's share of a frame split over GPUs) still runs launches of a whole frame's
+ * size; the step pipeline renders the frames one after another.  Stats are summed over the
+ * frames; sync as for rt_render_tiles; count_work calls must render one frame.  Replaces the
+ * reference's render loop (Code/raytracer.cpp:433-476) run once per frame. */
+int rt_render_frames(rt_scene_t scene, const rt_camera_desc* cam, const rt_render_params* params,
+                     const uint64_t* seeds, int32_t n_frames, const int32_t* tile_ids, int32_t n_tiles,
+                     int32_t tile_w, int32_t tile_h, float* d_rgb_out, void* stream, rt_stats* stats);
 
 /* Finishes the scene's last call made with rt_render_params.sync == 0: waits for it if it was
  * deferred (one-pass) and fills `stats` (may be null) -- also when that call had completed

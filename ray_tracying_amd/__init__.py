@@ -99,7 +99,7 @@ _host = None
 HIP_SYMBOLS = [
     "rt_device_count", "rt_scene_create", "rt_scene_destroy", "rt_render_tiles", "rt_malloc",
     "rt_free", "rt_memcpy_d2h", "rt_memcpy_h2d", "rt_synchronize", "rt_build_info", "rt_last_error",
-    "rt_quantise_device", "rt_tile_costs", "rt_tile_costs_measured", "rt_render_wait",
+    "rt_quantise_device", "rt_tile_costs", "rt_tile_costs_measured", "rt_render_wait", "rt_render_frames",
 ]
 HOST_SYMBOLS = [
     "rth_scene_load", "rth_scene_free", "rth_scene_get_info", "rth_scene_desc", "rth_scene_camera",
@@ -133,6 +133,9 @@ def _load():
     _hip.rt_render_tiles.argtypes = [c.c_void_p, c.POINTER(rt_camera_desc), c.POINTER(rt_render_params),
                                      c.POINTER(c.c_int32), c.c_int32, c.c_int32, c.c_int32, c.c_void_p,
                                      c.c_void_p, c.POINTER(rt_stats)]
+    _hip.rt_render_frames.argtypes = [c.c_void_p, c.POINTER(rt_camera_desc), c.POINTER(rt_render_params),
+                                      c.POINTER(c.c_uint64), c.c_int32, c.POINTER(c.c_int32), c.c_int32, c.c_int32,
+                                      c.c_int32, c.c_void_p, c.c_void_p, c.POINTER(rt_stats)]
     _hip.rt_malloc.argtypes = [c.c_int32, c.c_size_t, c.POINTER(c.c_void_p)]
     _hip.rt_free.argtypes = [c.c_void_p]
     _hip.rt_memcpy_d2h.argtypes = [c.c_void_p, c.c_void_p, c.c_size_t]
@@ -317,6 +320,22 @@ class DeviceScene:
                    "rt_render_tiles")
         return RenderStats.of(st)
 
+    def render_frames(self, seeds, tile_ids, tile_w: int, tile_h: int, d_out: int, params: RenderParams,
+                      stream: int | None = None) -> RenderStats:
+        """rt_render_frames: len(seeds) frames of the same tiles in one call (frame f with seed
+        seeds[f]; params.seed unused) into a DEVICE buffer of len(seeds) * len(tile_ids) tiles,
+        frame-major; frame f == render_tiles with seed seeds[f], bit for bit."""
+        ids = np.ascontiguousarray(np.asarray(tile_ids, dtype=np.int32))
+        sd = np.ascontiguousarray(np.asarray([int(x) & (2**64 - 1) for x in seeds], dtype=np.uint64))
+        p = params.c()
+        st = rt_stats()
+        _check_hip(_hip.rt_render_frames(self._h, ctypes.byref(self.cam), ctypes.byref(p),
+                                         sd.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), int(sd.size),
+                                         ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(ids.size),
+                                         int(tile_w), int(tile_h), ctypes.c_void_p(int(d_out)),
+                                         ctypes.c_void_p(int(stream) if stream else 0), ctypes.byref(st)),
+                   "rt_render_frames")
+        return RenderStats.of(st)
 
     def tile_costs(self, tile_w: int, tile_h: int) -> np.ndarray:
         """rt_tile_costs: per-tile cost estimate (projected primitive centres), tile id order."""

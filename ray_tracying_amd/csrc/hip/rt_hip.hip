@@ -39,6 +39,8 @@
 #include <vector>
 
 #include "rt_device.h"
+#include "rt_diag.h"  // diagnostic builds' hooks (RT_WD, RT_PT_*, RT_ET_*, diag_*): nothing in the product
+#include "rt_knobs.h"  // the runtime knobs (RT_* environment variables): one table, one snapshot per call
 
 using namespace rtd;
 
@@ -46,41 +48,31 @@ namespace {
 
 constexpr int kMaxDepth = 10;  // MAX_RECURSION_DEPTH, raytracer.hpp:11
 constexpr int kBlock = 256;
-// default LDS stack entries per lane (RT_LDS_STACK overrides): 12 for the traversal instances
-// that run 6 waves/SIMD (6 blocks x 24 KB of LDS per CU), 11 for the 7-wave ones (7 x 22 KB),
-// 16 for the one at 5 (fused point-light shadows over transformed shapes: its hit-record code
-// needs the registers)
+// default LDS stack entries per lane (RT_LDS_STACK overrides), by the instance's waves/SIMD
+// (instance_waves): 12 at 6 waves (6 blocks x 24 KB of LDS per CU) -- every instance but the two
+// below -- 11 at 7 (7 x 22 KB: the planes instances of whole frames), 16 at 5 (the soft-light
+// chains over transformed shapes; they keep runtime values capped at the tree's depth bound,
+// call_lds_entries)
 // the production traversal instances (kFixed) take the three loop parameters as constants
 // -- the defaults, the LDS stack per waves/SIMD -- so they hold no SGPRs of their own;
-// render_tiles launches them when a call's values are exactly these, else the runtime-knob
-// instances (RT_REFILL, RT_LEAF_MIN, RT_LDS_STACK, a tree shallower than the stack)
+// render_tiles launches them when a call's values are exactly these (any tree depth: a shallow
+// tree leaves the rows past its depth unused), else the runtime-knob instances (RT_REFILL,
+// RT_LEAF_MIN, RT_LDS_STACK, and the soft-light chains)
 constexpr int kSevenStack = 11, kRefillDefault = 48, kLeafDefault = 24;
 constexpr int default_stack(int waves) { return waves >= 7 ? kSevenStack : waves == 6 ? 12 : 16; }
-static int lds_stack_entries(int waves) {  // read per call: tests vary it within one process
-  const char* e = std::getenv("RT_LDS_STACK");
-  return e ? std::max(1, std::min(64, std::atoi(e))) : default_stack(waves);
-}
+static int lds_stack_entries(int waves) { return (int)knob(K_LDS_STACK, default_stack(waves)); }
 // LDS stack entries of a launch: the instance's default rows even for a tree shallower than
 // them (the rows past its depth stay unused; the kFixed instances assume the default), an
 // RT_LDS_STACK request -- and the soft-light chain instances, which keep runtime values and
 // whose 16 default rows at 5 waves/SIMD would fill a CU's LDS (C4 -0.9 %) -- capped at the
 // tree's depth bound
 static int call_lds_entries(int stack_bound, int waves, bool soft) {
-  return std::getenv("RT_LDS_STACK") || soft ? std::min(stack_bound, lds_stack_entries(waves)) : default_stack(waves);
+  return knob_set(K_LDS_STACK) || soft ? std::min(stack_bound, lds_stack_entries(waves)) : default_stack(waves);
 }
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
 constexpr int kCtlBytes = 4096;    // control block (cleared by init_kernel)
 constexpr int kStatsBytes = 512;
-// RT_WRITE_DIAG (diagnostic builds only): counts the traversal's HBM stores by kind -- stack
-// entries past the LDS rows (8 B), result words (4 B), hit records (32 B), occlusion words (4 B)
-// -- into control-block counters 80..83, printed per one-pass call (the PMC WRITE_SIZE
-// attribution)
-#ifdef RT_WRITE_DIAG
-#define RT_WD(k) atomicAdd(a.counters + 80 + (k), 1ull)
-#else
-#define RT_WD(k)
-#endif
 // scenes with fewer primitives spend their frame in the per-step passes over the slots, not in
 // traversal: their shadow rays are fused whatever the call size
 constexpr int kFuseFewPrims = 65536;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
@@ -92,6 +84,7 @@ constexpr int kCtrStride = 32;
 // reads their any_query copies.  Steps after the frame's last query find every slot-wave
 // retired (logic) and no query (trace) and return at once, so a batch may overshoot.
 constexpr int kMaxHostBatch = 16;
+constexpr int kMaxFrames = 1024;  // frames of one rt_render_frames call
 // Slot pipelines: the slots are split into independent logic -> trace pipelines on their own
 // streams, so one pipeline's logic step and launch tail overlap the other's traversal.
 constexpr int kPipes = 4;  // at most (RT_PIPES); the default is pipes_env()
@@ -216,7 +209,13 @@ struct LogicArgs {
   rt_camera_desc cam;
   int spp_sqrt, light_samples;
   uint64_t seed_key;
-  FastDiv fd_s;                 // sample -> (sj, si): division by spp_sqrt
+  // multi-frame calls (rt_render_frames): the call's tile list is the frames' lists end to end,
+  // frame f's output tiles at [f * frame_tiles, (f + 1) * frame_tiles) -- and frame f's samples
+  // keyed by seed_keys[f] instead of seed_key
+  int n_frames;
+  const uint64_t* seed_keys;
+  FastDiv fd_frame_tiles;
+  FastDiv fd_s;              // sample -> (sj, si): division by spp_sqrt
   double inv_s;                 // RN(1 / spp_sqrt): the jitter's quotients (rt_div_by)
   float inv_res_x, inv_res_y;   // RN(1 / res): the camera's pixel -> NDC quotients
   // work
@@ -318,9 +317,7 @@ struct TraceArgs {
   // their tiles by
   unsigned int* tile_cost;
   FastDiv fd_tile_units;
-#ifdef RT_EXIT_TIMING
-  unsigned long long* exit_log;  // diagnostic build: per wave (start, queue exhausted, exit) real time
-#endif
+  unsigned long long* exit_log;  // RT_EXIT_TIMING builds (rt_diag.h): per wave (start, queue exhausted, exit)
 };
 
 // ---------------------------------------------------------------- traversal
@@ -531,30 +528,44 @@ __device__ __forceinline__ bool pixel_coords(const LogicArgs& a, int p, int& x, 
 }
 
 // shade's specular term is m.specular * powf(ndh, shininess) (raytracer.cpp:245-250): with
-// every component of the specular colour zero it is +0 (or -0 for a -0 component) whatever
-// the finite, non-negative power is -- ndh = max(0, dot) never NaN, at most 1 + a few ulps,
-// shininess = 5 / r^2 <= 5e6 -- so the glibc powf restatement (~100 instructions, much of it
-// binary64) can be skipped: same bits.  The Blender scenes' materials (C3, C4) are all such.
-__device__ __forceinline__ bool spec_zero(const rt_material& m) {
-  return m.specular[0] == 0.0f && m.specular[1] == 0.0f && m.specular[2] == 0.0f;
-}
+// every component of the specular colour zero it is +0 (or -0 for a -0 component) whenever the
+// power is finite -- ndh = max(0, dot) is never NaN and at most 1 + a few ulps, so any shininess
+// in [0, 5e6] (the JSON loader's 5 / r^2, json_loader.cpp:56-61, lies in [5, 5e6]) -- and the
+// glibc powf restatement (~100 instructions, much of it binary64) can be skipped: same bits.
+// The Blender scenes' materials (C3, C4) are all such.  rt_scene_create decides it per
+// material on the host and marks the device copy (kMatSpecSkip in rt_material.pad): a C-ABI
+// caller's NaN, negative or huge shininess keeps the powf, and with it the reference's
+// 0 * inf = NaN.
+constexpr int32_t kMatSpecSkip = 1;
+__device__ __forceinline__ bool spec_zero(const rt_material& m) { return (m.pad & kMatSpecSkip) != 0; }
 
 // ---------------------------------------------------------------- logic kernel
-// unit -> (launch-local pixel, sample); false if the pixel lies outside the image
-__device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, int& px, int& py, int& sample) {
+// unit -> (launch-local pixel, sample) and the counter-RNG key of its frame; false if the pixel
+// lies outside the image
+// (frames = false: the step pipeline, whose calls render one frame -- rt_render_frames runs
+// them one after another)
+__device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, int& px, int& py, int& sample,
+                                            uint64_t& key, bool frames = true) {
   // units < 2^31 (checked on the host): 32-bit unsigned division
   const unsigned u = (unsigned)unit, ns = (unsigned)a.n_samples;
   const int p = (int)fdiv(u, a.fd_samples);
   sample = (int)(u - (unsigned)p * ns);
+  key = a.seed_key;
+  if (frames && a.n_frames > 1) {  // the frame of the unit's output tile
+    const int tl = (int)fdiv((uint32_t)p, a.fd_tile_px);
+    const int to = a.tile_out ? a.tile_out[tl] : tl;
+    key = a.seed_keys[fdiv((uint32_t)to, a.fd_frame_tiles)];
+  }
   size_t off;
   return pixel_coords(a, p, px, py, off);
 }
 
 // compute_pixel_color (raytracer.cpp:18-70): the camera ray of sample `sample` of pixel (px,
-// py) -- its RNG stream, the stratified jitter in double, Camera::pixelToRay_thin_lens (the
-// lens draws for an aperture > 0).  The ray's time is the caller's next draw.
-__device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, int sample, Rng& rng) {
-  rng.begin(a.seed_key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
+// py) -- its RNG stream (keyed by the frame's seed), the stratified jitter in double,
+// Camera::pixelToRay_thin_lens (the lens draws for an aperture > 0).  The ray's time is the
+// caller's next draw.
+__device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, int sample, uint64_t key, Rng& rng) {
+  rng.begin(key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
   const int s = a.spp_sqrt;
   float fx, fy;
   if (s <= 1) {
@@ -929,42 +940,7 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
 // `leaf_min` lanes wait on one (or no lane has a node to visit), then they all test their
 // leaf's primitives together -- leaf hits are sparse (~1 per 8 node visits per lane), and
 // testing them at once keeps the primitive code from running with a handful of lanes.
-// RT_PHASE_TIMING (diagnostic A/B builds only): per-wave s_memtime cycles spent in the refill,
-// leaf and node phases of trace_refill_kernel, and how often each runs, summed into the
-// control block (counters 64..71) and printed by rt_render_tiles.
-#ifdef RT_PHASE_TIMING
-// (and the lanes doing useful work: pt_l[k] lane-iterations of useful work, pt_w[k] the
-// wave's capacity -- 64 per node phase; 64 x the longest leaf per leaf phase, whose useful
-// work is the primitive tests)
-#define RT_PT_DECL                                                                                   \
-  unsigned long long pt_c[4] = {0, 0, 0, 0}, pt_n[4] = {0, 0, 0, 0}, pt_l[4] = {0, 0, 0, 0},        \
-                     pt_w[4] = {0, 0, 0, 0}, pt_t = __builtin_amdgcn_s_memtime();
-#define RT_PT_MARK(k)                                           \
-  do {                                                          \
-    const unsigned long long pt_now = __builtin_amdgcn_s_memtime(); \
-    pt_c[k] += pt_now - pt_t;                                   \
-    pt_n[k] += 1;                                               \
-    pt_t = pt_now;                                              \
-  } while (0)
-#define RT_PT_LANES(k, useful, capacity) \
-  do {                                   \
-    pt_l[k] += (useful);                 \
-    pt_w[k] += (capacity);               \
-  } while (0)
-#define RT_PT_FLUSH                                               \
-  if (lane == 0)                                                  \
-    for (int k = 0; k < 4; ++k) {                                 \
-      atomicAdd(ta.counters + 64 + k, pt_c[k]);                   \
-      atomicAdd(ta.counters + 68 + k, pt_n[k]);                   \
-      atomicAdd(ta.counters + 72 + k, pt_l[k]);                   \
-      atomicAdd(ta.counters + 76 + k, pt_w[k]);                   \
-    }
-#else
-#define RT_PT_DECL
-#define RT_PT_MARK(k)
-#define RT_PT_LANES(k, useful, capacity)
-#define RT_PT_FLUSH
-#endif
+// (RT_PHASE_TIMING builds split the waves' time into these phases: rt_diag.h.)
 #ifndef RT_TRACE_WAVES
 #define RT_TRACE_WAVES 6  // fused shadows over transformed shapes (C3; r05 A/B: 6 waves +4.2 % over 5
                           // once the hit record moved to settle and the planes to scalar fmas)
@@ -1191,10 +1167,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     }
   };
   RT_PT_DECL
-#ifdef RT_EXIT_TIMING
-  const unsigned long long et_begin = __builtin_amdgcn_s_memrealtime();
-  unsigned long long et_exh = 0;
-#endif
+  RT_ET_BEGIN
   for (;;) {
     RT_PT_MARK(3);  // loop control (ballots) since the node phase
     uint64_t act = __ballot(item != kNoItem);
@@ -1246,9 +1219,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
             }
             if (++sk >= (int)nfs) {
               exhausted = true;
-#ifdef RT_EXIT_TIMING
-              et_exh = __builtin_amdgcn_s_memrealtime();
-#endif
+              RT_ET_EXHAUSTED;
               break;
             }
           }
@@ -1277,17 +1248,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     // leaf phase: enough lanes wait on a leaf, or nothing else is left to do
     const uint64_t leafm = __ballot(is_leaf_item(item));
     if (leafm != 0ull && (popc_s(leafm) >= a.leaf_min || (act & ~leafm) == 0ull)) {
-#ifdef RT_PHASE_TIMING
-      {
-        const int c = is_leaf_item(item) ? (int)((uint32_t)item & 0x7fu) : 0;
-        int mx = c, sm = c;
-        for (int off = 32; off > 0; off >>= 1) {
-          mx = max(mx, __shfl_xor(mx, off));
-          sm += __shfl_xor(sm, off);
-        }
-        RT_PT_LANES(1, (unsigned long long)sm, 64ull * (unsigned long long)mx);
-      }
-#endif
+      RT_PT_LEAF_LANES;
       if (is_leaf_item(item)) {
         const uint32_t e = (uint32_t)item;
         test_prims<kCount, kPlanesOnly>(a, (int)((e & ~kLeafBit) >> 7), (int)(e & 0x7fu), q.r, q.any, q.tmax, q.par, true,
@@ -1298,15 +1259,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
       RT_PT_MARK(1);  // leaf phase
     }
     // node phase
-#ifdef RT_PHASE_TIMING
-    if (const uint64_t nm = __ballot(item >= 0)) {
-      RT_PT_LANES(2, (unsigned long long)__popcll(nm), 64ull);
-      if (item >= 0) item = node_visit<kCount, kPlanesOnly>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
-      RT_PT_MARK(2);  // node phase
-    }
-#else
+    RT_PT_NODE_BEGIN
     if (item >= 0) item = node_visit<kCount, kPlanesOnly>(a, q, lim, item, S, sw, gtid, nbox, dg_any_box, nvisit);
-#endif
+    RT_PT_NODE_END
   }
   // ---- drain (drain_help: the queue is dry).  A query still traversing keeps its lane (its
   // owner); a free lane becomes a helper: it takes the bottom entry of a busy lane's stack --
@@ -1423,14 +1378,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
     }
   }
   RT_PT_FLUSH
-#ifdef RT_EXIT_TIMING
-  if (lane == 0) {
-    unsigned long long* e = ta.exit_log + (size_t)(gtid >> 6) * 3;
-    e[0] = et_begin;
-    e[1] = et_exh;
-    e[2] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
+  RT_ET_END
   if (kCount && a.tile_cost) flush_tile_cost(a, lane, cost_tile, nvisit, nvc, nrays, nrc);
   trace_counters_out<kCount>(ta, lane, nrays, nbox, nprim, dg_any_rays, dg_any_box, nvisit);
 }
@@ -1858,13 +1806,14 @@ __global__ __launch_bounds__(kBlock) void camera_kernel(LogicArgs a) {
   const size_t N = (size_t)(unsigned)a.n_slots, u = (size_t)unit;
   float* Q = a.query;
   int px, py, sample;
-  if (!unit_coords(a, unit, px, py, sample)) {  // edge tile: pixel outside the image
+  uint64_t key;
+  if (!unit_coords(a, unit, px, py, sample, key)) {  // edge tile: pixel outside the image
     Q[(size_t)a.op_fk * N + u] = __int_as_float(-1);
     a.result[u] = -1;
     return;
   }
   Rng rng;
-  const Ray ray = sample_ray(a, px, py, sample, rng);
+  const Ray ray = sample_ray(a, px, py, sample, key, rng);
   Q[u] = ray.d.x;
   Q[N + u] = ray.d.y;
   Q[2 * N + u] = ray.d.z;
@@ -1920,7 +1869,8 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
     *a.any_query = 1u;
   }
   int px, py, sample;
-  if (!unit_coords(a, unit, px, py, sample)) {  // edge tile: pixel outside the image (stays idle)
+  uint64_t key;
+  if (!unit_coords(a, unit, px, py, sample, key, false)) {  // edge tile: pixel outside the image (stays idle)
     if (a.first_step) {
       S[F_UNIT * N + slot] = (uint32_t)-2;
       store_no_query(a.query, N, slot);
@@ -1928,7 +1878,7 @@ __global__ __launch_bounds__(kBlock, 8) void start_kernel(LogicArgs a) {
     return;
   }
   Rng rng;
-  Ray ray = sample_ray(a, px, py, sample, rng);
+  Ray ray = sample_ray(a, px, py, sample, key, rng);
   ray.time = (float)rng.next();
   S[F_UNIT * N + slot] = (uint32_t)unit;
   S[F_CTRL * N + slot] = (uint32_t)ST_CLOSEST;  // depth 0
@@ -2244,39 +2194,13 @@ void launch_trace(const TraceArgs& ta, bool count, bool planes, bool soft, bool 
   else if (fixed) launch_trace3<false, true>(ta, planes, soft, seven, blocks, lds, st);
   else launch_trace3<false, false>(ta, planes, soft, seven, blocks, lds, st);
 }
-static int pipes_env() {  // read per call: tests vary it within one process
-  const char* e = std::getenv("RT_PIPES");
-  return e ? std::max(1, std::min(kPipes, std::atoi(e))) : 1;
-}
-
-static int fetch_shards_env() {
-  static const int v = [] {
-    const char* e = std::getenv("RT_FETCH_SHARDS");
-    return e ? std::max(1, std::min(kMaxFetchShards, std::atoi(e))) : 32;  // r03 sweep: 4 / 8 / 16 / 32: 5377 / 5542 / 5628 / 5769 (headline)
-  }();
-  return v;
-}
-static int batch_shards_env() {
-  static const int v = [] {
-    const char* e = std::getenv("RT_BATCH_SHARDS");
-    return e ? std::max(1, std::min(kMaxBatchShards, std::atoi(e))) : 128;
-  }();
-  return v;
-}
-static int leaf_min_env() {
-  static const int v = [] {
-    const char* e = std::getenv("RT_LEAF_MIN");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : kLeafDefault;  // r03 sweep at 32M slots: 12 / 16 / 24 / 32 (two pipelines)
-  }();
-  return v;
-}
-static int refill_min_env() {
-  static const int v = [] {
-    const char* e = std::getenv("RT_REFILL");
-    return e ? std::max(1, std::min(64, std::atoi(e))) : kRefillDefault;
-  }();
-  return v;
-}
+static int pipes_env() { return (int)knob(K_PIPES, 1); }
+// r03 sweep: 4 / 8 / 16 / 32 fetch shards: 5377 / 5542 / 5628 / 5769 Mrays/s (headline)
+static int fetch_shards_env() { return (int)knob(K_FETCH_SHARDS, 32); }
+static int batch_shards_env() { return (int)knob(K_BATCH_SHARDS, 128); }
+// r03 sweep at 32M slots: leaf 12 / 16 / 24 / 32 (two pipelines); DESIGN.md 5
+static int leaf_min_env() { return (int)knob(K_LEAF_MIN, kLeafDefault); }
+static int refill_min_env() { return (int)knob(K_REFILL, kRefillDefault); }
 
 void launch_logic(const LogicArgs& la, bool frames, bool refr, bool tex, bool planes, unsigned blocks, hipStream_t st) {
   if (frames && refr) {
@@ -2335,6 +2259,9 @@ struct rt_scene_s {
   void* d_ctl = nullptr;  // bytes 16/24: box/prim tests, 32: rays (u64), 240..: diagnostics, 488: node visits
   int* d_tiles = nullptr;
   size_t tiles_cap = 0;
+  uint64_t* d_keys = nullptr;  // a multi-frame call's per-frame counter-RNG keys
+  size_t cap_keys = 0;
+  std::vector<uint64_t> keys_on_device;
   // (each array grown on demand by grow(); its byte capacity beside it: a one-pass call needs
   // only the query record, result, hit record and occlusion bits of its slots)
   uint32_t* d_state = nullptr;
@@ -2379,9 +2306,7 @@ struct rt_scene_s {
     int n_tiles = 0, tiles_x = 0, tiles_y = 0;
     std::vector<int32_t> tl_dev;
     std::vector<unsigned char> meas_key;
-#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING) || defined(RT_WRITE_DIAG)
-    TraceArgs ta{};
-#endif
+    TraceArgs ta{};  // the launch's arguments (diagnostic builds' reports, rt_diag.h)
   } pending;
   // a call with rt_render_params.sync == 0 that completed before returning (the step pipeline,
   // or a call split into tile chunks): its statistics, handed out by the next rt_render_wait
@@ -2466,7 +2391,7 @@ static void tile_cost_order(rt_scene_s* s, const rt_camera_desc* cam, int tile_w
                             const int32_t* tile_ids, int n_tiles, bool wanted, std::vector<int32_t>& order) {
   order.resize((size_t)n_tiles);
   for (int i = 0; i < n_tiles; ++i) order[i] = i;
-  if (const char* e = std::getenv("RT_TILE_ORDER")) wanted = std::atoi(e) != 0;  // 0 / 1: never / always
+  wanted = knob(K_TILE_ORDER, wanted) != 0;  // 0 / 1: never / always
   if (!wanted || n_tiles < 2) return;
   if (s->cost_pts.empty()) return;
   const std::vector<float>& cost = tile_costs(s, cam, tile_w, tile_h, tiles_x, tiles_y);
@@ -2555,7 +2480,7 @@ int rt_scene_destroy(rt_scene_t s) {
   (void)hipDeviceSynchronize();
   free_workspace(s);
   void* ptrs[] = {s->d_prims, s->d_nodes, s->d_mats, s->d_lights, s->d_tex, s->d_texels, s->d_ctl, s->d_tiles,
-                  s->d_prim_refs, s->d_ref_boxes, s->d_spill, s->d_batch_ctr, s->d_fetch};
+                  s->d_prim_refs, s->d_ref_boxes, s->d_spill, s->d_batch_ctr, s->d_fetch, s->d_keys};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
@@ -2577,6 +2502,7 @@ int rt_scene_destroy(rt_scene_t s) {
 }
 
 int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
+  knobs_refresh();
   if (!d || !out) return fail(RT_EINVAL, "rt_scene_create: null argument");
   if (d->n_prims < 0 || d->n_prims >= (1 << 24) || (d->n_prims > 0 && (!d->prims || !d->prim_refs)) ||
       (d->n_prims > d->n_unbounded && (d->n_nodes <= 0 || !d->nodes)) || d->n_unbounded < 0 ||
@@ -2640,12 +2566,20 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
                    d->n_lights >= 1 && d->n_lights <= 24 ? d->n_lights : 0;
   s->late_draws = s->soft_lights;
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
+  // the device copy of the materials: pad = kMatSpecSkip where shade's specular term is +-0 for
+  // any hit (spec_zero); the caller's pad is ignored
+  std::vector<rt_material> mats(d->materials, d->materials + d->n_materials);
+  for (rt_material& m : mats)
+    m.pad = m.specular[0] == 0.0f && m.specular[1] == 0.0f && m.specular[2] == 0.0f && m.shininess >= 0.0f &&
+                    m.shininess <= 5e6f
+                ? kMatSpecSkip
+                : 0;
   int rc = RT_OK;
   if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
       (rc = upload_nodes(&s->d_nodes, d->nodes, d->n_nodes, d->prim_stride == 64)) ||
       (rc = upload(&s->d_prim_refs, d->prim_refs, (size_t)d->n_prims * sizeof(rt_prim_ref))) ||
       (rc = upload(&s->d_ref_boxes, d->ref_leaf_boxes, (size_t)d->n_ref_leaves * 8 * sizeof(float))) ||
-      (rc = upload(&s->d_mats, d->materials, (size_t)d->n_materials * sizeof(rt_material))) ||
+      (rc = upload(&s->d_mats, mats.data(), mats.size() * sizeof(rt_material))) ||
       (rc = upload(&s->d_lights, d->lights, (size_t)d->n_lights * sizeof(rt_light))) ||
       (rc = upload(&s->d_tex, d->textures, (size_t)d->n_textures * sizeof(rt_texture))) ||
       (rc = upload(&s->d_texels, d->texels, (size_t)d->n_texel_bytes))) {
@@ -2678,7 +2612,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
       const size_t lds_bytes = (size_t)lds_entries * kBlock * 2 * sizeof(int);  // (entry, t_near) per stack slot
       int b = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, lds_bytes) != hipSuccess || b < 1) b = 2;
-      if (const char* e = std::getenv("RT_TRACE_BPC")) b = std::max(1, std::min(b, std::atoi(e)));  // diagnostic
+      b = std::min(b, (int)knob(K_TRACE_BPC, b));  // diagnostic cap
       return b;
     };
     bpc = occupancy(planes ? (const void*)trace_refill_kernel<false, true, false, false>
@@ -2738,43 +2672,6 @@ int rt_tile_costs(rt_scene_t s, const rt_camera_desc* cam, int32_t tile_w, int32
 
 }  // extern "C"
 
-#ifdef RT_EXIT_TIMING
-// diagnostic build: wave start / queue-exhausted / exit times of a trace launch (100 MHz clock)
-static int print_exit_log(const TraceArgs& ta, float ms, int step) {
-  const int nw = (int)ta.n_threads / 64;
-  std::vector<unsigned long long> lg((size_t)nw * 3);
-  HIP_TRY(hipMemcpy(lg.data(), ta.exit_log, lg.size() * 8, hipMemcpyDeviceToHost), RT_EDEVICE);
-  unsigned long long b0 = ~0ull, x0 = ~0ull;
-  std::vector<double> ex;
-  for (int w = 0; w < nw; ++w) {
-    b0 = std::min(b0, lg[(size_t)w * 3]);
-    if (lg[(size_t)w * 3 + 1]) x0 = std::min(x0, lg[(size_t)w * 3 + 1]);
-  }
-  for (int w = 0; w < nw; ++w) ex.push_back((double)(lg[(size_t)w * 3 + 2] - b0) * 1e-5);  // ms
-  std::sort(ex.begin(), ex.end());
-  std::fprintf(stderr, "[rt exit] step %2d: trace %.3f ms; queue exhausted at %.3f ms; waves exit: 10%% %.3f, 50%% %.3f, 90%% %.3f, 99%% %.3f, last %.3f ms\n",
-               step, ms, x0 == ~0ull ? -1.0 : (double)(x0 - b0) * 1e-5, ex[nw / 10], ex[nw / 2], ex[nw * 9 / 10],
-               ex[nw * 99 / 100], ex[nw - 1]);
-  return RT_OK;
-}
-#endif
-
-#ifdef RT_PHASE_TIMING
-// diagnostic build: the traversal waves' time per phase (s_memtime ticks, executions) and the
-// lane utilisation of the node and leaf phases
-static int print_phase_timing(const unsigned long long* counters) {
-  unsigned long long pt[16] = {};
-  HIP_TRY(hipMemcpy(pt, counters + 64, sizeof(pt), hipMemcpyDeviceToHost), RT_EDEVICE);
-  const double tot = (double)(pt[0] + pt[1] + pt[2] + pt[3]);
-  std::fprintf(stderr, "[rt phase] refill %.3f (%llu), leaf %.3f (%llu), node %.3f (%llu), control %.3f (%llu) of %.3g wave-ticks; "
-               "lane utilisation: leaf %.3f (%.4g prim tests), node %.3f (%.4g visits)\n",
-               pt[0] / tot, pt[4], pt[1] / tot, pt[5], pt[2] / tot, pt[6], pt[3] / tot, pt[7], tot,
-               pt[13] ? (double)pt[9] / (double)pt[13] : 0.0, (double)pt[9], pt[14] ? (double)pt[10] / (double)pt[14] : 0.0,
-               (double)pt[10]);
-  return RT_OK;
-}
-#endif
-
 // Finishes the scene's enqueued one-pass call: waits for its last event, records its measured
 // tile costs (instrumented calls) and fills `stats` (may be null).
 static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
@@ -2795,21 +2692,10 @@ static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
   }
   float ms = 0.f, t_a = 0.f, t_b = 0.f, k_ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, s->ev_a[0][0], s->ev_b[0][0]), RT_EDEVICE);
-#ifdef RT_EXIT_TIMING
-  if (const int rc = print_exit_log(q.ta, ms, 0)) return rc;
-#endif
-#ifdef RT_PHASE_TIMING
-  if (const int rc = print_phase_timing(q.ta.counters)) return rc;
-#endif
-#ifdef RT_WRITE_DIAG
-  {
-    unsigned long long wd[4] = {};
-    HIP_TRY(hipMemcpy(wd, q.ta.counters + 80, sizeof(wd), hipMemcpyDeviceToHost), RT_EDEVICE);
-    std::fprintf(stderr, "[rt writes] HBM stack entries %llu (%.3f GB), result words %llu (%.3f GB), hit records %llu "
-                 "(%.3f GB), occlusion words %llu (%.3f GB)\n", wd[0], wd[0] * 8e-9, wd[1], wd[1] * 4e-9, wd[2],
-                 wd[2] * 32e-9, wd[3], wd[3] * 4e-9);
+  if (kDiagBuild) {
+    diag_after_launch(q.ta, ms, 0);
+    diag_after_call(q.ta.counters, true);
   }
-#endif
   s->last_iters = 1;
   if (!stats) return RT_OK;
   *stats = rt_stats{};
@@ -2843,25 +2729,18 @@ static bool one_pass_scene(const rt_scene_s* s) {
   return !frames && !s->soft_lights && (s->desc.n_lights == 0 || s->fuse_lights == s->desc.n_lights) &&
          (s->desc.prim_stride == 64 || !tex);
 }
-static bool one_pass_env() {
-  if (const char* e = std::getenv("RT_ONE_PASS")) return std::atoi(e) != 0;
-  return true;
-}
+static bool one_pass_env() { return knob(K_ONE_PASS, 1) != 0; }
 static void note_ignored_knobs() {
   static std::atomic<bool> said[4] = {};
-  static const char* const knobs[4] = {"RT_SLOTS", "RT_PIPES", "RT_FUSE", "RT_DIAG"};
+  static const Knob knobs[4] = {K_SLOTS, K_PIPES, K_FUSE, K_DIAG};
   for (int k = 0; k < 4; ++k)
-    if (std::getenv(knobs[k]) && !said[k].exchange(true))
+    if (knob_set(knobs[k]) && !said[k].exchange(true))
       std::fprintf(stderr, "librt_hip: %s applies to the step pipeline only; one-pass calls ignore it "
-                   "(RT_ONE_PASS=0 selects the step pipeline)\n", knobs[k]);
+                   "(RT_ONE_PASS=0 selects the step pipeline)\n", kKnobDefs[knobs[k]].name);
 }
 // units of one one-pass call (larger calls run as tile chunks): 52 B of workspace per unit
 // touched (query direction 12, result 4, hit record 32 on a hit, occlusion bits 4)
-static long long one_pass_cap() {
-  long long cap = 1LL << 30;
-  if (const char* e = std::getenv("RT_ONE_PASS_MAX")) cap = std::max(1LL, std::min(cap, std::atoll(e)));
-  return cap;
-}
+static long long one_pass_cap() { return knob(K_ONE_PASS_MAX, 1LL << 30); }
 
 extern "C" {
 
@@ -2890,19 +2769,24 @@ int rt_tile_costs_measured(rt_scene_t s, const rt_camera_desc* cam, int32_t tile
 }  // extern "C"
 
 static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
-                        int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr, rt_stats* stats);
+                        int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr, rt_stats* stats,
+                        const uint64_t* seeds, int n_frames);
 
 extern "C" {
 
 // A call with sync == 0 is finished by rt_render_wait, whichever path ran: a deferred one-pass
 // call is waited for there; a call that completed before returning (the step pipeline, tile
-// chunks) leaves its statistics for it (held), so the caller's wait never reads zeros.
-int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
-                    int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
-                    rt_stats* stats) {
+// chunks) leaves its statistics for it (held), so the caller's wait never reads zeros.  The
+// statistics are gathered only when someone reads them: the caller (stats) or that wait.
+static int render_entry(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
+                        int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr, rt_stats* stats,
+                        const uint64_t* seeds, int n_frames) {
+  knobs_refresh();
   if (s) s->held = false;
   rt_stats st{};
-  const int rc = render_tiles(s, cam, p, tile_ids, n_tiles, tile_w, tile_h, d_out, stream_ptr, &st);
+  const bool want = stats || (p && p->sync == 0);
+  const int rc = render_tiles(s, cam, p, tile_ids, n_tiles, tile_w, tile_h, d_out, stream_ptr, want ? &st : nullptr,
+                              seeds, n_frames);
   if (rc == RT_OK && p->sync == 0 && !s->pending.active) {
     s->held = true;
     s->held_stats = st;
@@ -2911,11 +2795,37 @@ int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_par
   return rc;
 }
 
+int rt_render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
+                    int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
+                    rt_stats* stats) {
+  return render_entry(s, cam, p, tile_ids, n_tiles, tile_w, tile_h, d_out, stream_ptr, stats, nullptr, 1);
+}
+
+int rt_render_frames(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const uint64_t* seeds,
+                     int32_t n_frames, const int32_t* tile_ids, int32_t n_tiles, int32_t tile_w, int32_t tile_h,
+                     float* d_out, void* stream_ptr, rt_stats* stats) {
+  if (n_frames < 1 || n_frames > kMaxFrames || !seeds)
+    return fail(RT_EINVAL, "rt_render_frames: need 1.." + std::to_string(kMaxFrames) + " frames and their seeds");
+  return render_entry(s, cam, p, tile_ids, n_tiles, tile_w, tile_h, d_out, stream_ptr, stats, seeds, n_frames);
+}
+
 }  // extern "C"
+
+static void add_stats(rt_stats& acc, const rt_stats& st) {
+  acc.rays += st.rays;
+  acc.box_tests += st.box_tests;
+  acc.prim_tests += st.prim_tests;
+  acc.node_visits += st.node_visits;
+  acc.kernel_ms += st.kernel_ms;
+  acc.trace_ms += st.trace_ms;
+  acc.trace_busy_ms += st.trace_busy_ms;
+  acc.iterations += st.iterations;
+  if (st.path != RT_PATH_ONE_PASS) acc.path = RT_PATH_STEPS;
+}
 
 static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render_params* p, const int32_t* tile_ids,
                         int32_t n_tiles, int32_t tile_w, int32_t tile_h, float* d_out, void* stream_ptr,
-                        rt_stats* stats) {
+                        rt_stats* stats, const uint64_t* seeds, int n_frames) {
   if (!s || !cam || !p || (!tile_ids && n_tiles > 0) || !d_out) return fail(RT_EINVAL, "rt_render_tiles: null argument");
   if (tile_w <= 0 || tile_h <= 0 || tile_w % 8 || tile_h % 8)
     return fail(RT_EINVAL, "rt_render_tiles: tile size must be a positive multiple of 8");
@@ -2929,14 +2839,50 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     if (const int rc = finish_one_pass(s, nullptr)) return rc;
   if (stats) *stats = rt_stats{};
   if (n_tiles == 0) return RT_OK;
+  rt_render_params pf = *p;  // a multi-frame call's single frames: params with the frame's seed
+  std::vector<int32_t> frame_list;  // a multi-frame call's tile list: the frames' lists end to end
+  const int frame_tiles = n_tiles;
   {  // calls larger than the unit cap run as consecutive tile chunks (same pixels: the counter
      // RNG keys every sample by pixel, so the split changes no value); the per-sample colour
      // buffer (12 B per unit) stays bounded, and the frame-wide 2^31 unit limit goes away
     const long long per_tile = (long long)tile_w * tile_h * (p->spp_sqrt <= 1 ? 1LL : (long long)p->spp_sqrt * p->spp_sqrt);
     long long cap = 1LL << 30;
-    if (const char* e = std::getenv("RT_MAX_UNITS")) cap = std::max(1LL, std::min(cap, std::atoll(e)));
-    if (one_pass_scene(s) && one_pass_env()) cap = std::min(cap, one_pass_cap());
-    if (n_tiles > 1 && (long long)n_tiles * per_tile > cap) {
+    cap = knob(K_MAX_UNITS, cap);
+    const bool op = one_pass_scene(s) && one_pass_env();
+    if (op) cap = std::min(cap, one_pass_cap());
+    const size_t frame_floats = (size_t)n_tiles * tile_w * tile_h * 3;
+    if (n_frames > 1) {
+      // Multi-frame calls (rt_render_frames): a one-pass scene renders as many frames per pass as
+      // the unit cap holds -- every one of their samples in one camera pass, one traversal launch
+      // and one shading pass, so a rank's share of a split frame runs launches of the whole
+      // frame's size.  The step pipeline renders the frames one after another.
+      const int per_pass = op ? (int)std::max(1LL, std::min<long long>(n_frames, cap / ((long long)n_tiles * per_tile))) : 1;
+      if (per_pass < n_frames) {
+        rt_stats acc{};
+        acc.path = RT_PATH_ONE_PASS;
+        rt_render_params pc = *p;
+        pc.sync = 1;  // the passes share the workspace: each one finishes before the next
+        for (int f0 = 0; f0 < n_frames; f0 += per_pass) {
+          const int nf = std::min(per_pass, n_frames - f0);
+          rt_stats st{};
+          pc.seed = seeds[f0];
+          const int rc = render_tiles(s, cam, &pc, tile_ids, n_tiles, tile_w, tile_h, d_out + (size_t)f0 * frame_floats,
+                                      stream_ptr, stats ? &st : nullptr, seeds + f0, nf);
+          if (rc) return rc;
+          add_stats(acc, st);
+        }
+        if (stats) *stats = acc;
+        return RT_OK;
+      }
+      frame_list.resize((size_t)n_frames * n_tiles);
+      for (int f = 0; f < n_frames; ++f) std::copy(tile_ids, tile_ids + n_tiles, frame_list.begin() + (size_t)f * n_tiles);
+      tile_ids = frame_list.data();
+      n_tiles *= n_frames;
+    } else if (seeds) {
+      pf.seed = seeds[0];
+      p = &pf;
+    }
+    if (n_frames == 1 && n_tiles > 1 && (long long)n_tiles * per_tile > cap) {
       const int k = (int)std::max(1LL, std::min<long long>(n_tiles, cap / per_tile));
       rt_stats acc{};
       acc.path = RT_PATH_ONE_PASS;
@@ -2945,22 +2891,17 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
       for (int t0 = 0; t0 < n_tiles; t0 += k) {
         rt_stats st{};
         const int rc = render_tiles(s, cam, &pc, tile_ids + t0, std::min(k, n_tiles - t0), tile_w, tile_h,
-                                    d_out + (size_t)t0 * tile_w * tile_h * 3, stream_ptr, &st);
+                                    d_out + (size_t)t0 * tile_w * tile_h * 3, stream_ptr, stats ? &st : nullptr,
+                                    nullptr, 1);
         if (rc) return rc;
-        acc.rays += st.rays;
-        acc.box_tests += st.box_tests;
-        acc.prim_tests += st.prim_tests;
-        acc.node_visits += st.node_visits;
-        acc.kernel_ms += st.kernel_ms;
-        acc.trace_ms += st.trace_ms;
-        acc.trace_busy_ms += st.trace_busy_ms;
-        acc.iterations += st.iterations;
-        if (st.path != RT_PATH_ONE_PASS) acc.path = RT_PATH_STEPS;
+        add_stats(acc, st);
       }
       if (stats) *stats = acc;
       return RT_OK;
     }
   }
+  if (n_frames > 1 && p->count_work)
+    return fail(RT_EINVAL, "rt_render_frames: instrumented (count_work) calls render one frame");
   const long long n_pixels_ll = (long long)n_tiles * tile_w * tile_h;
   if (n_pixels_ll > 0x7fffffffLL) return fail(RT_EINVAL, "rt_render_tiles: too many pixels in one call");
   const int n_pixels = (int)n_pixels_ll;
@@ -2987,7 +2928,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   const bool one_pass = one_pass_scene(s) && one_pass_env() && n_units <= one_pass_cap();
   if (one_pass) note_ignored_knobs();
   long long slots = frames_scene ? std::min(n_units, 6LL << 20) : std::min(n_units, 128LL << 20);
-  if (const char* e = std::getenv("RT_SLOTS")) slots = std::max(1LL << 12, std::atoll(e));
+  slots = knob(K_SLOTS, slots);
   // slot-state words are addressed S[field * N + slot] in 32-bit int: (highest field + 1) * N
   // <= 2^31.  Scenes without Trace frames touch fields up to F_RAY + 2 (the ray origin), scenes
   // with frames all F_COUNT; RT_SLOTS is clamped to that bound (one-pass calls keep no slot
@@ -3080,6 +3021,21 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   }
   la.light_samples = p->light_samples;
   la.seed_key = mix64_host(p->seed + 0x9E3779B97F4A7C15ull);
+  la.n_frames = n_frames;
+  la.fd_frame_tiles = make_fastdiv((uint32_t)frame_tiles);
+  la.seed_keys = nullptr;
+  if (n_frames > 1) {  // frame f's key, as a single-frame call with seed seeds[f] derives it
+    std::vector<uint64_t> keys((size_t)n_frames);
+    for (int f = 0; f < n_frames; ++f) keys[f] = mix64_host(seeds[f] + 0x9E3779B97F4A7C15ull);
+    if (keys.size() * 8 > s->cap_keys) s->keys_on_device.clear();
+    if (const int rc = grow(s->d_keys, s->cap_keys, keys.size() * 8)) return rc;
+    if (s->keys_on_device != keys) {
+      s->keys_on_device = keys;
+      HIP_TRY(hipMemcpyAsync(s->d_keys, s->keys_on_device.data(), keys.size() * 8, hipMemcpyHostToDevice, stream),
+              RT_EDEVICE);
+    }
+    la.seed_keys = s->d_keys;
+  }
   la.tile_ids = s->d_tiles;
   la.tile_out = identity ? nullptr : s->d_tiles + n_tiles;
   // affine tile lists (one GPU: 0, 1, 2 ...; round-robin ranks: r, r + N ...) need no lookup
@@ -3115,9 +3071,9 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // (RT_SOFT_FUSE=0), or by the logic kernel itself (RT_SOFT_FUSE=0 RT_SHADOW_STEP=0)
   const bool soft_scene = s->soft_lights && p->light_samples > 1;
   bool soft_trace = soft_scene;
-  if (const char* e = std::getenv("RT_SOFT_FUSE")) soft_trace = soft_trace && std::atoi(e) != 0;
+  soft_trace = soft_trace && knob(K_SOFT_FUSE, 1) != 0;
   la.multi_shadow = soft_scene && !soft_trace ? 1 : 0;
-  if (const char* e = std::getenv("RT_SHADOW_STEP")) la.multi_shadow = la.multi_shadow && std::atoi(e) != 0;
+  la.multi_shadow = la.multi_shadow && knob(K_SHADOW_STEP, 1) != 0;
   la.wave_done = s->d_wave_done;
   la.batch_ctr = s->d_batch_ctr;
   // every shard needs a slot-wave to drain it (wave w claims from shard w % batch_shards)
@@ -3136,7 +3092,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   ta.fetch_shards = fetch_shards_env();
   ta.xcd_chunk = RT_XCD_CHUNK_DEFAULT;
-  if (const char* e = std::getenv("RT_XCD_CHUNK")) ta.xcd_chunk = std::min(std::max(0, std::atoi(e)), 1 << 20) & ~3;  // 32-bit group indices
+  ta.xcd_chunk = (int)knob(K_XCD_CHUNK, ta.xcd_chunk) & ~3;  // at most 2^20: 32-bit group indices
   ta.wave_done = s->d_wave_done;
   ta.rays = (unsigned long long*)(ctl + 8);  // byte 32
   ta.n_slots = n_slots;
@@ -3144,13 +3100,13 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // the refill kernel's leaf items hold first << 7 in 31 bits
   ta.refill_min = refill_min_env();
   ta.leaf_min = leaf_min_env();
-  ta.diag = std::getenv("RT_DIAG") != nullptr ? 1 : 0;
+  ta.diag = knob(K_DIAG, 0) != 0 ? 1 : 0;
   // free lanes help the queries still traversing once a launch's queue is dry (RT_DRAIN_HELP=0 off)
   // The instrumented (count_work) frame runs without helpers: a helper searches a subtree under
   // a bound that lags its owner's, so its visits depend on scheduling; without them the counts
   // are the serial near-first traversal's (the algorithmic bytes bench.py reports)
   ta.drain_help = p->count_work ? 0 : 1;
-  if (const char* e = std::getenv("RT_DRAIN_HELP")) ta.drain_help = std::atoi(e) != 0 ? 1 : 0;
+  ta.drain_help = (int)knob(K_DRAIN_HELP, ta.drain_help);
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
   for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
@@ -3158,7 +3114,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // the closest hit starts its shade loop in the tracing lane too: planes, or untextured
   // transformed shapes (that lane computes point and normal, not (u, v)); RT_SOFT_START=0 off
   ta.soft_start = soft_trace && s->desc.n_lights >= 1 && (planes_only || !(s->desc.flags & RT_SCENE_HAS_TEXTURE)) ? 1 : 0;
-  if (const char* e = std::getenv("RT_SOFT_START")) ta.soft_start = ta.soft_start && std::atoi(e) != 0;
+  ta.soft_start = ta.soft_start && knob(K_SOFT_START, 1) != 0;
   ta.frames = need_frames ? 1 : 0;
   ta.pinhole = cam->aperture <= 0.0f ? 1 : 0;
   // Fused shadow rays halve the steps of a sample.  They pay when the call is small (at most
@@ -3168,10 +3124,11 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // camera and shadow rays interleave within a wave and lose coherence (headline -6.5 %).
   // RT_FUSE=0 / 1 overrides (1: whenever the scene allows it).
   ta.n_fuse = n_units <= 2LL * n_slots || s->desc.n_prims < kFuseFewPrims ? s->fuse_lights : 0;
-  if (const char* e = std::getenv("RT_FUSE"))  // (a one-pass call traces every point light's shadow ray fused)
-    if (!one_pass) ta.n_fuse = std::atoi(e) != 0 ? s->fuse_lights : 0;
-  // the launched instance (launch_trace3): fused, soft or plain; 6 waves/SIMD and 12 LDS stack
-  // entries except fused shadows over transformed shapes (5, 16)
+  if (knob_set(K_FUSE) && !one_pass)  // (a one-pass call traces every point light's shadow ray fused)
+    ta.n_fuse = knob(K_FUSE, 0) != 0 ? s->fuse_lights : 0;
+  // the launched instance (launch_trace3): fused, soft or plain, at instance_waves() waves/SIMD
+  // with default_stack() LDS rows (7 / 11 for whole planes-only frames, 5 / 16 for soft-light
+  // chains over transformed shapes, else 6 / 12)
   ta.one_pass = one_pass ? 1 : 0;
   ta.tile_cost = nullptr;
   const bool measure_tiles = one_pass && p->count_work;
@@ -3200,10 +3157,10 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // eighth -2.6 %) and smaller calls keep six.  RT_TRACE_SEVEN=0 / 1 overrides (1: every planes
   // call but soft-light and instrumented ones).
   bool seven = planes_only && !soft_launch && !p->count_work && p->sync != 0 && n_units > (32LL << 20);
-  if (const char* e = std::getenv("RT_TRACE_SEVEN"))
-    seven = planes_only && !soft_launch && !p->count_work && std::atoi(e) != 0;
-  // the 7-wave instances have the default loop parameters built in: another stack depth (a
-  // shallow tree, RT_LDS_STACK) or threshold (RT_REFILL, RT_LEAF_MIN) takes the 6-wave ones
+  if (knob_set(K_TRACE_SEVEN)) seven = planes_only && !soft_launch && !p->count_work && knob(K_TRACE_SEVEN, 0) != 0;
+  // the 7-wave instances have the default loop parameters built in: another stack depth
+  // (RT_LDS_STACK) or threshold (RT_REFILL, RT_LEAF_MIN) takes the 6-wave runtime-knob ones (a
+  // shallow tree keeps the default rows, call_lds_entries, and so keeps seven)
   if (seven && (call_lds_entries(s->desc.stack_bound, 7, false) != kSevenStack || ta.refill_min != kRefillDefault ||
                 ta.leaf_min != kLeafDefault))
     seven = false;
@@ -3213,6 +3170,12 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // SGPRs, C4 -0.8 %)
   const bool fixed = !soft_launch && ta.lds_entries == default_stack(trace_waves) && ta.refill_min == kRefillDefault &&
                      ta.leaf_min == kLeafDefault;
+  if (knob(K_LOG_INSTANCE, 0) != 0)  // which trace_refill_kernel instance this call launches (knob tests)
+    std::fprintf(stderr, "[rt instance] %s, %lld units, %d frame(s): waves %d, lds rows %d (stack bound %d: %d rows "
+                 "spill to HBM), %s%s, %s\n", one_pass ? "one-pass" : "steps", n_units, n_frames, trace_waves,
+                 ta.lds_entries, s->desc.stack_bound, std::max(0, s->desc.stack_bound - ta.lds_entries),
+                 planes_only ? "planes" : "transformed", fuse_launch ? " fused" : soft_launch ? " soft" : "",
+                 fixed ? "constant loop parameters" : "runtime loop parameters");
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
   la.occl = s->d_occl;
@@ -3220,14 +3183,10 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // entry + t_near per stack slot
   const size_t lds = (size_t)ta.lds_entries * kBlock * 2 * sizeof(int);
 
-  const bool diag = std::getenv("RT_DIAG") != nullptr && !p->count_work;
-  const bool steps_log = std::getenv("RT_STEPS_LOG") != nullptr;  // diagnostic: every trace launch, any pipeline
+  const bool diag = knob(K_DIAG, 0) != 0 && !p->count_work;
+  const bool steps_log = knob(K_STEPS_LOG, 0) != 0;  // diagnostic: every trace launch, any pipeline
   // the diagnostics wait on every step (one pipeline)
-#ifdef RT_EXIT_TIMING
-  const bool step_sync = true;
-#else
-  const bool step_sync = diag;
-#endif
+  const bool step_sync = diag || kDiagStepSync;
 
   // ---- pipelines: the slots may split into independent logic -> trace sequences, one per
   // stream (units are claimed from the shared batch counters, so the split changes no value):
@@ -3240,8 +3199,8 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // refraction: many short steps, a logic step ~25 % of each) take two since r05, with 6M slots
   // between them (C4, same box, 3 reps: one pipeline of 16M 13531-13563 Mrays/s, two of 6M
   // 14135-14190, two of 8M 14044-14185, two of 12M 13691-13721, three of 12M 13886-13963).
-  int n_pipes = n_units <= (4LL << 20) ? 1 : frames_scene && !std::getenv("RT_PIPES") ? 2 : pipes_env();
-  if (const char* e = std::getenv("RT_PIPES")) n_pipes = pipes_env();  // an explicit request holds for any size
+  int n_pipes = n_units <= (4LL << 20) ? 1 : frames_scene && !knob_set(K_PIPES) ? 2 : pipes_env();
+  if (knob_set(K_PIPES)) n_pipes = pipes_env();  // an explicit request holds for any size
   if (step_sync || one_pass) n_pipes = 1;
   n_pipes = std::max(1, std::min(n_pipes, n_slots / kBlock));  // every pipeline gets whole blocks of slots
   struct Pipe {
@@ -3268,7 +3227,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // 4918-4924 / 5404-5440).  RT_DEFER_BPC overrides.
   int defer_free = one_pass && p->sync == 0 ? 1 : 0;
   if (one_pass && p->sync == 0)
-    if (const char* e = std::getenv("RT_DEFER_BPC")) defer_free = std::max(0, std::atoi(e));
+    defer_free = (int)knob(K_DEFER_BPC, defer_free);
   const unsigned grid_cap = (unsigned)std::max(
       1, s->n_cu * std::max(1, (n_units <= (4LL << 20) ? std::max(1, call_bpc - 1) : call_bpc) - defer_free));
   size_t spill_need = 0;
@@ -3304,11 +3263,12 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     pipes[h].ta.spill = s->d_spill + (size_t)2 * off;
     off += spill_entries * pipes[h].ta.n_threads;
   }
-#ifdef RT_EXIT_TIMING
-  static unsigned long long* exit_log = nullptr;
-  if (!exit_log) HIP_TRY(hipMalloc(&exit_log, (size_t)1 << 22), RT_ENOMEM);  // 512 K u64: 170 K waves
-  for (int h = 0; h < n_pipes; ++h) pipes[h].ta.exit_log = exit_log;
-#endif
+  if (kDiagBuild) {
+    TraceArgs tas[kPipes];
+    for (int h = 0; h < n_pipes; ++h) tas[h] = pipes[h].ta;
+    if (!diag_prepare(tas, n_pipes)) return fail(RT_ENOMEM, "diagnostic exit log");
+    for (int h = 0; h < n_pipes; ++h) pipes[h].ta.exit_log = tas[h].exit_log;
+  }
 
   {
     InitArgs ia{};
@@ -3388,9 +3348,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     q.tiles_y = tiles_y;
     q.tl_dev = tl_dev;
     q.meas_key = meas_key_of(cam, tile_w, tile_h, n_samples);
-#if defined(RT_EXIT_TIMING) || defined(RT_PHASE_TIMING) || defined(RT_WRITE_DIAG)
     q.ta = P.ta;
-#endif
     // sync == 0: deferred -- rt_render_wait (or the scene's next call) finishes it, so the
     // caller can enqueue another frame (on another scene handle and stream) meanwhile
     if (p->sync == 0) {
@@ -3450,9 +3408,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
             hipEventElapsedTime(&t_b, s->ev_t0, s->ev_b[h][k]) == hipSuccess)
           busy.emplace_back(t_a, t_b);
         const bool more = flag[(size_t)k * kFetchStride] != 0;
-#ifdef RT_EXIT_TIMING
-        if (more) print_exit_log(P.ta, ms, iters);
-#endif
+        if (kDiagBuild && more) diag_after_launch(P.ta, ms, iters);
         if (diag && more) {
           unsigned long long rc = 0;
           HIP_TRY(hipMemcpy(&rc, ctl + 8, 8, hipMemcpyDeviceToHost), RT_EDEVICE);
@@ -3504,12 +3460,10 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     stats->trace_busy_ms = un;
     stats->iterations = iters;
     stats->path = one_pass ? RT_PATH_ONE_PASS : RT_PATH_STEPS;
-#ifdef RT_PHASE_TIMING
-    if (const int rc = print_phase_timing((unsigned long long*)(ctl + 4))) return rc;
-#endif
+    if (kDiagBuild) diag_after_call((const unsigned long long*)(ctl + 4), false);
     stats->node_visits = 0;
     if (p->count_work) stats->node_visits = h_stats[61];  // lane-level node visits (trace_counters_out, ctl byte 488)
-    if (p->count_work && std::getenv("RT_DIAG")) {
+    if (p->count_work && knob(K_DIAG, 0) != 0) {
       unsigned long long dg[2] = {0, 0};
       HIP_TRY(hipMemcpy(dg, ctl + 128, sizeof(dg), hipMemcpyDeviceToHost), RT_EDEVICE);
       const unsigned long long cr = cnt[2] - dg[0], cb = cnt[0] - dg[1];

@@ -57,6 +57,23 @@ def test_gpus_flag_spawns_ranks(n):
     assert rk["render_ms_per_step"] == [float(r + 1) for r in range(n)]
     assert rk["slowest_rank"] == n - 1 and rk["slowest_render_ms_per_step"] == float(n)
     assert rk["fastest_render_ms_per_step"] == 1.0
+    # the CPU baseline is timed (by rank 0) at every N, not only at N = 1,
+    # and the roofline's frac is the guide's VALU peak (frac_vs_spec), the chip-measured one beside it
+    assert d["cpu_baseline_rank"] == 0
+    v = d["roofline_valu"]
+    assert v is not None and v["frac"] == v["frac_vs_spec"]
+    assert v["spec_peak"] == pytest.approx(256 * 2 * 64 * 2.4 / 1e3, rel=1e-3)
+    assert v["frac_vs_measured"] > v["frac"]  # the measured peak (1.73 per CU-cycle) is below the spec
+
+
+def test_cpu_baseline_rank_and_valu_block():
+    import types
+    assert bench.cpu_baseline_rank(types.SimpleNamespace(no_cpu_baseline=False)) == 0
+    assert bench.cpu_baseline_rank(types.SimpleNamespace(no_cpu_baseline=True)) is None
+    pv = {"valu_g_wave_instr_per_s": 640.0, "lane_utilisation": 0.5, "label": "x"}
+    v = bench.valu_block(pv, os.path.join(ROOT, "profiles", "x.json"), 1.733, "ubench")
+    assert v["achieved"] == pytest.approx(640.0 * 64 * 0.5 / 1e3, rel=1e-6)
+    assert v["frac"] == v["frac_vs_spec"] == pytest.approx(v["achieved"] / 78.6432, rel=1e-3)
 
 
 def test_world_size_mismatch_fails():

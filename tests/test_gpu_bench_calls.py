@@ -4,8 +4,8 @@ The other full-scale parity tests render a few tiles per call.  The timed calls 
 headline step is one one-pass call over all 256 tiles of the 1024^2 x 100 spp frame (104.9M
 units, costliest tiles first, their outputs remapped to the caller's order); C5 is one call of
 2^30 units over the whole 4096^2 x 64 spp frame (64-bit query offsets, ~56 GB of workspace);
-a rank's share of an 8-way split is rendered with two frames in flight, deferred, on two scene
-handles and streams.  Each test runs bench.py itself (`--dump-frame`: after the timed steps the
+a rank's share of an 8-way split is rendered eight frames per rt_render_frames call (r06; two
+frames in flight on two scene handles and streams until r05).  Each test runs bench.py itself (`--dump-frame`: after the timed steps the
 frame at --seed is rendered by the same calls -- same frames in flight, issued behind another
 frame still in flight -- and saved) and compares it with the oracle (counter RNG) bit for bit
 (r05: the C3 and C4 frames as timed too -- C4 on the step pipeline's two slot pipelines):
@@ -80,9 +80,10 @@ def test_headline_frame_as_timed(soup1024, tmp_path, gpu):
 
 def test_rank_share_as_timed(soup1024, tmp_path, gpu):
     """One rank's share of the 8-way split (rank 7: 32 tiles of the lattice deal) rendered as its
-    rank does: two frames in flight, deferred, on two scene handles and streams."""
+    rank does (r06): eight frames per rt_render_frames call -- one camera pass, one traversal
+    launch of the whole frame's size, one shading pass -- the frame at --seed the last of them."""
     img, line = _bench(tmp_path, "em8", "--emulate", "8", "--emulate-rank", "7")
-    assert line["config"]["frames_in_flight"] == 2
+    assert line["config"]["frames_per_call"] == 8 and line["config"]["frames_in_flight"] == 1
     mine = [int(t) for t in tl.assign_tiles(256, 8, 7, 16)]
     assert len(mine) == 32
     done = np.isfinite(img).all(axis=2)

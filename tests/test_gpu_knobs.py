@@ -12,6 +12,7 @@ caller's order instead of costliest first (small calls' default), and the lanes 
 traversing when a launch's queue runs dry left alone instead of helped by the free lanes.
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -62,10 +63,11 @@ KNOBS = [
     {"RT_DRAIN_HELP": "1", "RT_LDS_STACK": "2", "RT_LEAF_MIN": "1"},  # helpers take entries from the HBM spill area
     {"RT_DRAIN_HELP": "0", **STEPS},  # the step pipeline without helpers
     {"RT_TRACE_SEVEN": "1"},  # the 7-wave planes instances (whole frames' default) on a small call
-    {"RT_TRACE_SEVEN": "1", "RT_LDS_STACK": "3", **STEPS},  # ... through the step pipeline, deep stacks spilling
+    {"RT_TRACE_SEVEN": "1", **STEPS},  # ... through the step pipeline (fused shadows: the soup is small)
     {"RT_XCD_CHUNK": "0"},  # the round-robin deal of the work queue (group g to shard g % 32)
     {"RT_XCD_CHUNK": "4", **STEPS},  # the smallest XCD chunks, through the step pipeline
     {"RT_XCD_CHUNK": "100000"},  # one chunk larger than the call: one XCD's shards, the rest stolen
+    {"RT_XCD_CHUNK": "1048576"},  # the clamp bound (2^20 groups per chunk)
     # step-pipeline knobs on a one-pass scene: ignored (one message each), still one-pass
     {"RT_FUSE": "1"},
     {"RT_FUSE": "0", "RT_SLOTS": "4096", "RT_PIPES": "2", "RT_DIAG": "1"},
@@ -96,3 +98,33 @@ def test_knobs_do_not_change_results(scene, tmp_path, gpu):
             for k in ("RT_SLOTS", "RT_PIPES", "RT_FUSE", "RT_DIAG"):
                 if k in env:
                     assert f"librt_hip: {k} applies to the step pipeline only" in r.stderr, (env, k)
+
+
+def test_seven_wave_unfused_instance(tmp_path, gpu):
+    """the non-fused 7-wave planes instance (trace_refill_kernel<false, true, false,
+    false, true, true>) -- production launches it for light-less whole frames and for step-pipeline
+    planes calls whose shadows are not fused -- through the step pipeline with RT_FUSE=0 and
+    RT_TRACE_SEVEN=1, on a 60K-triangle soup whose tree is deeper than the instance's 11 LDS rows
+    (entries past them go to the HBM spill area), and a light-less soup through the one-pass path;
+    the instance log (RT_LOG_INSTANCE) must show the 7-wave unfused launch, and the frame must equal
+    the oracle's."""
+    cases = [(scenes.soup(60000, seed=31, res=(48, 40)), {"RT_ONE_PASS": "0", "RT_FUSE": "0"}, "steps"),
+             (scenes.soup(60000, seed=32, res=(48, 40), light=False), {}, "one-pass")]
+    for k, (sc, env, kind) in enumerate(cases):
+        p = scenes.write(sc, str(tmp_path / f"deep{k}.json"))
+        ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=5, spp_sqrt=2, light_samples=2, use_bvh=True,
+                                texture_root=scenes.TEXTURES)
+        out = str(tmp_path / f"deep{k}.npy")
+        r = subprocess.run([sys.executable, "-c", CHILD, ROOT, p, out, scenes.TEXTURES],
+                           env={**os.environ, **env, "RT_TRACE_SEVEN": "1", "RT_LOG_INSTANCE": "1"},
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        inst = [ln for ln in r.stderr.splitlines() if ln.startswith("[rt instance]")]
+        assert inst and all(f"[rt instance] {kind}," in ln for ln in inst), r.stderr[-2000:]
+        assert all("waves 7, lds rows 11" in ln and "planes," in ln and "fused" not in ln and "soft" not in ln
+                   for ln in inst), inst
+        spill = [int(re.search(r"stack bound \d+: (\d+) rows spill", ln).group(1)) for ln in inst]
+        assert min(spill) > 0, inst  # the tree's stack bound exceeds the 11 LDS rows
+        img = np.load(out)
+        assert int((img.view(np.uint32) != ref.view(np.uint32)).sum()) == 0, kind
+        assert int(r.stdout.strip().splitlines()[-1]) == ost["rays"]

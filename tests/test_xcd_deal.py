@@ -20,7 +20,7 @@ def shard_seq(block: int):
     return [((block % X + sk // P) % X) + X * ((block // X + sk % P) % P) for sk in range(NFS)]
 
 
-@pytest.mark.parametrize("xc", [4, 64, 512])
+@pytest.mark.parametrize("xc", [4, 64, 512, 1 << 20])
 @pytest.mark.parametrize("n_groups", [1, 5, 63, 64, 65, 1000, 4099])
 def test_every_group_once(xc, n_groups):
     seen = []
