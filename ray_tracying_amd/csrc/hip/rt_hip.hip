@@ -119,6 +119,8 @@ struct HitRec {
   uint32_t mat;
 };
 __device__ __forceinline__ float* hit_rec(float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
+// TraceArgs::has_tex: what a closest hit leaves for the shading (finish_query)
+constexpr int kHitRecord = 0, kHitTex = 1, kHitCompact = 2;
 __device__ __forceinline__ const float* hit_rec(const float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
 __device__ __forceinline__ const float* hit_rec_u(const float* hit, size_t unit) { return hit + unit * HIT_STRIDE; }
 // point + normal + material
@@ -290,7 +292,8 @@ struct TraceArgs {
   unsigned long long* counters;  // box tests, prim tests (count_work)
   float* hit;                 // [n_slots][HIT_STRIDE]: attributes of a closest hit (for the logic step)
   float2* hit_uv;             // [n_slots]: (u, v) of a closest hit, textured scenes
-  int has_tex;                // some material is textured: hit u, v needed
+  int has_tex;                // hit output: kHitRecord (32-B record), kHitTex (some material is textured:
+                              // the record and (u, v)), kHitCompact (one-pass planes calls: t alone)
   int refill_min;             // refill kernel: refill finished lanes when fewer than this many traverse
   int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
   int diag;                   // count_work under RT_DIAG: wave-level utilisation counters
@@ -620,6 +623,9 @@ __device__ __forceinline__ void complete_query(const TraceArgs& a, int slot, con
 // written once here: Plane::intersect's hit point o + t d from the best t (the same ops as the
 // test, so the same bits) and the record's precomputed normal (shapes.cpp:472-480) and
 // material -- in hp / hn too, for a fused shadow ray that follows (returns true then).
+// kHitCompact (one-pass planes-only calls without textures, at most one fused light: r06): only
+// the hit's t, 4 B instead of the 32-B record -- shade_reduce_kernel rebuilds the record from t,
+// the unit's query record and the primitive (compact_hit) with the same ops.
 // Transformed shapes get their record from the lane's settle (fused / soft-start instances) or
 // the logic step.
 template <bool kCount, bool kPlanesOnly>
@@ -629,17 +635,21 @@ __device__ __forceinline__ bool finish_query(const TraceArgs& a, int slot, const
   complete_query<kCount, kPlanesOnly>(a, slot, q, h, nprim);
   a.result[slot] = q.any ? (h.done ? 1 : 0) : h.best_idx;
   RT_WD(1);
-  if (kPlanesOnly && !a.has_tex && !q.any && h.best_idx >= 0) {
+  // (an opaque copy, compared here: compares hoisted to the kernel's entry stay live across the
+  // traversal loop in SGPRs of their own -- 2 to 6 more spilled)
+  const int hit_mode = kPlanesOnly ? sgpr_copy(a.has_tex) : a.has_tex;
+  if (kPlanesOnly && hit_mode != kHitTex && !q.any && h.best_idx >= 0) {
     RT_WD(2);
     const float4* rec = at_byte(a.c.prims, (uint32_t)h.best_idx * ((uint32_t)a.c.prim_stride4 << 4));  // < 2^24
     const float* w = reinterpret_cast<const float*>(rec);
     hn = V3{w[3], w[7], w[11]};
     const uint32_t tag = __float_as_uint(w[15]);
     hp = V3{r.o.x + h.best_t * r.d.x, r.o.y + h.best_t * r.d.y, r.o.z + h.best_t * r.d.z};
-    store_hit_pnm(hit_rec(a.hit, slot), hp, hn, RT_TAG_MATERIAL(tag));
+    if (hit_mode == kHitCompact) a.hit[slot] = h.best_t;
+    else store_hit_pnm(hit_rec(a.hit, slot), hp, hn, RT_TAG_MATERIAL(tag));
     return true;
   }
-  if (kPlanesOnly && a.has_tex && !q.any && h.best_idx >= 0) {
+  if (kPlanesOnly && hit_mode == kHitTex && !q.any && h.best_idx >= 0) {
     // textured planes: the hit record with (u, v) -- the same primitive test with attributes,
     // on the primitive this lane just tested (cached).  Scenes with transformed shapes get
     // their record from the logic step (logic_kernel, ST_CLOSEST): sphere / cube / rectangle
@@ -2061,7 +2071,25 @@ __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit, i
 #endif
 constexpr int kSrPixels = RT_SR_PIXELS, kSrChunk = 8, kSrStride = kSrChunk * 3 + 1;  // odd row: conflict-free sums
 constexpr int kSrUnits = kSrPixels * kSrChunk / kBlock;                     // units per thread per pass
-template <bool kTex>
+// kHitCompact calls (r06): the hit record finish_query used to store, rebuilt here from what the
+// trace kernel keeps -- the hit's t -- and what the call already holds: the unit's camera ray
+// (origin the camera's location or the stored lens origin, direction from the query record) and
+// the plane record's precomputed normal and tag.  The point is o + t d with the trace kernel's own
+// ops on the same operands, so the same bits.
+__device__ __forceinline__ HitRec compact_hit(const LogicArgs& a, size_t unit, int res) {
+  const size_t N = (size_t)(unsigned)a.n_slots;
+  const float t = a.hit[unit];
+  const float* w = reinterpret_cast<const float*>(a.c.prims) + (size_t)(unsigned)res * 16;  // 64-B plane records
+  V3 o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
+  if (a.op_fo >= 0) {
+    const float* Qo = a.query + (size_t)a.op_fo * N + unit;
+    o = V3{Qo[0], Qo[N], Qo[2 * N]};
+  }
+  const V3 d{a.query[unit], a.query[N + unit], a.query[2 * N + unit]};
+  return HitRec{V3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z}, V3{w[3], w[7], w[11]}, 0.0f, 0.0f,
+                RT_TAG_MATERIAL(__float_as_uint(w[15]))};
+}
+template <bool kTex, bool kCompact>
 __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(LogicArgs a) {
   __shared__ float stage[kSrPixels * kSrStride];
   const int p0 = blockIdx.x * kSrPixels;
@@ -2084,7 +2112,10 @@ __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(Logic
     }
     HitRec hr[kSrUnits];
 #pragma unroll
-    for (int m = 0; m < kSrUnits; ++m) hr[m] = res[m] >= 0 ? load_hit(hit_rec_u(a.hit, u[m])) : HitRec{};
+    for (int m = 0; m < kSrUnits; ++m) {
+      if constexpr (kCompact) hr[m] = res[m] >= 0 ? compact_hit(a, u[m], res[m]) : HitRec{};
+      else hr[m] = res[m] >= 0 ? load_hit(hit_rec_u(a.hit, u[m])) : HitRec{};
+    }
 #pragma unroll
     for (int m = 0; m < kSrUnits; ++m) {
       if ((int)threadIdx.x + m * kBlock < total) {
@@ -3089,7 +3120,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.result = s->d_result;
   ta.hit = s->d_hit;
   ta.hit_uv = s->d_hit_uv;
-  ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
+  ta.has_tex = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0 ? kHitTex : kHitRecord;
   ta.fetch_shards = fetch_shards_env();
   ta.xcd_chunk = RT_XCD_CHUNK_DEFAULT;
   ta.xcd_chunk = (int)knob(K_XCD_CHUNK, ta.xcd_chunk) & ~3;  // at most 2^20: 32-bit group indices
@@ -3178,6 +3209,11 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
                  fixed ? "constant loop parameters" : "runtime loop parameters");
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
+  // one-pass planes-only calls without textures and with at most one fused light keep only the
+  // hit's t (kHitCompact; a later light's shadow ray would reload the full record); RT_COMPACT_HIT=0
+  // keeps the 32-B record
+  if (one_pass && planes_only && ta.has_tex == kHitRecord && ta.n_fuse <= 1 && knob(K_COMPACT_HIT, 1) != 0)
+    ta.has_tex = kHitCompact;
   la.occl = s->d_occl;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
   // entry + t_near per stack slot
@@ -3331,8 +3367,10 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
     const unsigned rblocks = (unsigned)((n_pixels + kSrPixels - 1) / kSrPixels);
-    if (tex) hipLaunchKernelGGL(shade_reduce_kernel<true>, dim3(rblocks), dim3(kBlock), 0, stream, la);
-    else hipLaunchKernelGGL(shade_reduce_kernel<false>, dim3(rblocks), dim3(kBlock), 0, stream, la);
+    if (tex) hipLaunchKernelGGL((shade_reduce_kernel<true, false>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+    else if (ta.has_tex == kHitCompact)
+      hipLaunchKernelGGL((shade_reduce_kernel<false, true>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+    else hipLaunchKernelGGL((shade_reduce_kernel<false, false>), dim3(rblocks), dim3(kBlock), 0, stream, la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     if (measure_tiles)

@@ -54,7 +54,8 @@ def _frames_vs_single(path, spp_sqrt, ids, seeds, env=None, light_samples=1):
             st = ds.render_tiles(ids, T, T, buf.data_ptr(), p)
             single.append(buf.cpu().numpy().copy())
             rays += st.rays
-        multi = torch.full((len(seeds) * n,), float("nan"), dtype=torch.float32, device="cuda:0")
+        # (pixels of edge tiles outside the image are left untouched: zero in both buffers)
+        multi = torch.zeros(len(seeds) * n, dtype=torch.float32, device="cuda:0")
         p.seed = 12345  # not used by rt_render_frames
         st = ds.render_frames(seeds, ids, T, T, multi.data_ptr(), p)
         got = multi.cpu().numpy().reshape(len(seeds), n)
