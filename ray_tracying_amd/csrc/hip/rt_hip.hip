@@ -244,6 +244,7 @@ struct LogicArgs {
   int* result;           // [n_slots] (shadow_step_kernel marks consumed results)
   float* hit;            // [n_slots][HIT_STRIDE] (closest hits; written here for transformed shapes)
   float2* hit_uv;        // [n_slots] (u, v) of closest hits in textured scenes
+  const float4* prim_shade;  // planes-only scenes: per primitive (normal, material) -- compact hits (compact_hit)
   int late_draws;        // some step after a sample's start draws random numbers (soft lights, glossy)
   int pinhole;           // camera aperture <= 0: primary rays start at the camera location
   int multi_shadow;      // soft lights, light_samples > 1, RT_SOFT_FUSE=0: shadow_step_kernel runs first
@@ -2079,15 +2080,14 @@ constexpr int kSrUnits = kSrPixels * kSrChunk / kBlock;                     // u
 __device__ __forceinline__ HitRec compact_hit(const LogicArgs& a, size_t unit, int res) {
   const size_t N = (size_t)(unsigned)a.n_slots;
   const float t = a.hit[unit];
-  const float* w = reinterpret_cast<const float*>(a.c.prims) + (size_t)(unsigned)res * 16;  // 64-B plane records
+  const float4 ns = a.prim_shade[res];  // the plane's normal and material (rt_scene_create)
   V3 o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
   if (a.op_fo >= 0) {
     const float* Qo = a.query + (size_t)a.op_fo * N + unit;
     o = V3{Qo[0], Qo[N], Qo[2 * N]};
   }
   const V3 d{a.query[unit], a.query[N + unit], a.query[2 * N + unit]};
-  return HitRec{V3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z}, V3{w[3], w[7], w[11]}, 0.0f, 0.0f,
-                RT_TAG_MATERIAL(__float_as_uint(w[15]))};
+  return HitRec{V3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z}, V3{ns.x, ns.y, ns.z}, 0.0f, 0.0f, __float_as_uint(ns.w)};
 }
 template <bool kTex, bool kCompact>
 __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(LogicArgs a) {
@@ -2278,6 +2278,7 @@ struct rt_scene_s {
   void* d_tex = nullptr;
   void* d_texels = nullptr;
   void* d_prim_refs = nullptr;
+  float4* d_prim_shade = nullptr;  // planes-only scenes: per primitive (normal, material) for compact hits
   void* d_ref_boxes = nullptr;
   int n_cu = 0, trace_blocks_per_cu = 0;  // plain traversal instance
   int trace_blocks_per_cu_fuse = 0, trace_blocks_per_cu_soft = 0;  // shadow-chain instances (kFuse / kSoft)
@@ -2511,7 +2512,8 @@ int rt_scene_destroy(rt_scene_t s) {
   (void)hipDeviceSynchronize();
   free_workspace(s);
   void* ptrs[] = {s->d_prims, s->d_nodes, s->d_mats, s->d_lights, s->d_tex, s->d_texels, s->d_ctl, s->d_tiles,
-                  s->d_prim_refs, s->d_ref_boxes, s->d_spill, s->d_batch_ctr, s->d_fetch, s->d_keys};
+                  s->d_prim_refs, s->d_ref_boxes, s->d_spill, s->d_batch_ctr, s->d_fetch, s->d_keys,
+                  s->d_prim_shade};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->h_flag) (void)hipHostFree(s->h_flag);
@@ -2597,6 +2599,22 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
                    d->n_lights >= 1 && d->n_lights <= 24 ? d->n_lights : 0;
   s->late_draws = s->soft_lights;
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
+  // planes-only scenes: what the shading of a compact hit needs of its plane, 16 B per primitive --
+  // the precomputed normal and the material index (record words 3, 7, 11 and the tag's bits)
+  std::vector<float4> prim_shade;
+  if (d->prim_stride == 64) {
+    prim_shade.resize((size_t)d->n_prims);
+    const float* P = reinterpret_cast<const float*>(d->prims);
+    for (int32_t i = 0; i < d->n_prims; ++i) {
+      const float* a = P + (size_t)i * 16;
+      uint32_t tag;
+      std::memcpy(&tag, a + 15, 4);
+      const uint32_t mat = RT_TAG_MATERIAL(tag);
+      float matf;
+      std::memcpy(&matf, &mat, 4);
+      prim_shade[i] = make_float4(a[3], a[7], a[11], matf);
+    }
+  }
   // the device copy of the materials: pad = kMatSpecSkip where shade's specular term is +-0 for
   // any hit (spec_zero); the caller's pad is ignored
   std::vector<rt_material> mats(d->materials, d->materials + d->n_materials);
@@ -2609,6 +2627,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   if ((rc = upload(&s->d_prims, d->prims, (size_t)d->n_prims * d->prim_stride)) ||
       (rc = upload_nodes(&s->d_nodes, d->nodes, d->n_nodes, d->prim_stride == 64)) ||
       (rc = upload(&s->d_prim_refs, d->prim_refs, (size_t)d->n_prims * sizeof(rt_prim_ref))) ||
+      (rc = upload((void**)&s->d_prim_shade, prim_shade.data(), prim_shade.size() * sizeof(float4))) ||
       (rc = upload(&s->d_ref_boxes, d->ref_leaf_boxes, (size_t)d->n_ref_leaves * 8 * sizeof(float))) ||
       (rc = upload(&s->d_mats, mats.data(), mats.size() * sizeof(rt_material))) ||
       (rc = upload(&s->d_lights, d->lights, (size_t)d->n_lights * sizeof(rt_light))) ||
@@ -3037,6 +3056,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   c.eps_abs = 1e-5f * (s->desc.scene_scale > 1.0f ? s->desc.scene_scale : 1.0f);
   la.c = c;
   la.mats = (const rt_material*)s->d_mats;
+  la.prim_shade = s->d_prim_shade;
   la.lights = (const rt_light*)s->d_lights;
   la.n_lights = s->desc.n_lights;
   la.textures = (const rt_texture*)s->d_tex;
