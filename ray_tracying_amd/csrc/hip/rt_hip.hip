@@ -1610,18 +1610,23 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
             vis = vis / (float)ns;
             if (!(vis <= 0.0f)) {
               V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
-              V3 V = normalize(sub(ray.o, hp));
               V3 lc = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
               float dsq = dot(lc, lc);
               float ldist = sqrtf(dsq);
               V3 Ld = normalize(lc);
               float ndl = smax(0.0f, dot(hn, Ld));
               V3 diff = mul(base, ndl);
-              V3 H = normalize(add(Ld, V));
-              float ndh = smax(0.0f, dot(hn, H));
               // a material without a specular colour adds 0 * si == +0 for every finite si >= 0
-              // (ndh in [0, 1 + eps], shininess <= 5e6): the same bits without the powf
-              float si = spec_zero(m) ? 0.0f : rt_powf(ndh, m.shininess);
+              // (ndh in [0, 1 + eps], shininess <= 5e6): the same bits without the powf -- and
+              // without the view and half vectors, which feed nothing else (r06: their two
+              // normalisations, six divisions, are skipped too)
+              float si = 0.0f;
+              if (!spec_zero(m)) {
+                V3 V = normalize(sub(ray.o, hp));
+                V3 H = normalize(add(Ld, V));
+                float ndh = smax(0.0f, dot(hn, H));
+                si = rt_powf(ndh, m.shininess);
+              }
               V3 spec{m.specular[0] * si, m.specular[1] * si, m.specular[2] * si};
               float att = (10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq);
               V3 inner{diff.x * m.k_diffuse + spec.x * m.k_specular, diff.y * m.k_diffuse + spec.y * m.k_specular,
@@ -2033,16 +2038,19 @@ __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit, i
       vis = vis / (float)1;  // ns = 1 (radius 0)
       if (!(vis <= 0.0f)) {
         V3 base = kTex ? diffuse_color(a, m, hu, hv) : V3{m.diffuse[0], m.diffuse[1], m.diffuse[2]};
-        V3 V = normalize(sub(ro, hp));
         V3 lc = sub(V3{L.location[0], L.location[1], L.location[2]}, hp);
         float dsq = dot(lc, lc);
         float ldist = sqrtf(dsq);
         V3 Ld = normalize(lc);
         float ndl = smax(0.0f, dot(hn, Ld));
         V3 diff = mul(base, ndl);
-        V3 H = normalize(add(Ld, V));
-        float ndh = smax(0.0f, dot(hn, H));
-        float si = spec_zero(m) ? 0.0f : rt_powf(ndh, m.shininess);  // as in logic_kernel
+        float si = 0.0f;  // as in logic_kernel: V and H only when the specular term is not +-0
+        if (!spec_zero(m)) {
+          V3 V = normalize(sub(ro, hp));
+          V3 H = normalize(add(Ld, V));
+          float ndh = smax(0.0f, dot(hn, H));
+          si = rt_powf(ndh, m.shininess);
+        }
         V3 spec{m.specular[0] * si, m.specular[1] * si, m.specular[2] * si};
         float att = (10.0f * L.intensity) / (25.0f + 10.0f * ldist + 150.0f * dsq);
         V3 inner{diff.x * m.k_diffuse + spec.x * m.k_specular, diff.y * m.k_diffuse + spec.y * m.k_specular,
