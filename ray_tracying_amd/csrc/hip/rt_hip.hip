@@ -2292,6 +2292,7 @@ struct rt_scene_s {
   int trace_blocks_per_cu_fuse = 0, trace_blocks_per_cu_soft = 0;  // shadow-chain instances (kFuse / kSoft)
   int trace_blocks_per_cu_seven = 0, trace_blocks_per_cu_fuse_seven = 0;  // 7-wave planes instances
   bool late_draws = false;  // a light with radius > 0 or a rough material: draws after a sample's start
+  bool moving = false;      // some sphere has a non-zero velocity: the ray time matters
   bool soft_lights = false;  // a light with radius > 0 (several shadow samples with -light_sample > 1)
   int* d_spill = nullptr;
   size_t spill_cap = 0;
@@ -2577,10 +2578,14 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   }
   // RT_TAG_TRI1_NEVER changes what a[12] means (a squared radius, not c3.x): only on a valid
   // Plane record, with a finite non-negative radius
+  bool moving = false;
   for (int32_t i = 0; i < d->n_prims; ++i) {
     const float* a = reinterpret_cast<const float*>(d->prims) + (size_t)i * (d->prim_stride / 4);
     uint32_t tag;
     std::memcpy(&tag, a + 15, 4);
+    // (from the velocity itself, not the tag: a caller's untagged moving sphere still gets its time)
+    moving = moving || (d->prim_stride == 128 && RT_TAG_KIND(tag) == RT_PRIM_SPHERE &&
+                        (a[12] != 0.0f || a[13] != 0.0f || a[14] != 0.0f));
     if ((tag & RT_TAG_TRI1_NEVER) &&
         !(RT_TAG_KIND(tag) == RT_PRIM_PLANE && (tag & RT_TAG_PLANE_VALID) && std::isfinite(a[12]) && a[12] >= 0.0f))
       return fail(RT_EINVAL, "rt_scene_create: RT_TAG_TRI1_NEVER on a record that is not a valid Plane with a[12] >= 0");
@@ -2606,6 +2611,7 @@ int rt_scene_create(int32_t device, const rt_scene_desc* d, rt_scene_t* out) {
   s->fuse_lights = (d->prim_stride == 64 || !(s->desc.flags & RT_SCENE_HAS_TEXTURE)) && !s->soft_lights &&
                    d->n_lights >= 1 && d->n_lights <= 24 ? d->n_lights : 0;
   s->late_draws = s->soft_lights;
+  s->moving = moving;
   for (int i = 0; i < d->n_materials; ++i) s->late_draws = s->late_draws || d->materials[i].roughness > 0.0f;
   // planes-only scenes: what the shading of a compact hit needs of its plane, 16 B per primitive --
   // the precomputed normal and the material index (record words 3, 7, 11 and the tag's bits)
@@ -3008,7 +3014,11 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   int op_fields = 3, op_fo = -1, op_ft = -1, op_fk = -1;
   if (one_pass) {
     if (cam->aperture > 0.0f) op_fo = op_fields, op_fields += 3;  // thin lens: the origin
-    if (!planes_only) op_ft = op_fields++;  // a plane ignores the ray time (a moving sphere needs it)
+    // the ray time: only a moving sphere reads it (every other primitive, a static sphere included,
+    // gives the same bits for any time >= 0: its velocity terms are +-0), and it is the sample's
+    // last draw in a one-pass call -- so scenes without one skip the draw and its 4 B per unit
+    // (r06: C3's camera rays)
+    if (!planes_only && s->moving) op_ft = op_fields++;
     bool edge = false;  // some tile reaches past the image: its outside units are marked in a kind word
     for (int i = 0; i < n_tiles && !edge; ++i)
       edge = ((tile_ids[i] % tiles_x) + 1) * tile_w > cam->res_x || ((tile_ids[i] / tiles_x) + 1) * tile_h > cam->res_y;
