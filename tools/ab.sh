@@ -22,9 +22,9 @@ B=tests/golden/scenes/blend
 args_for() {
   case "$1" in
     head) echo "--steps 10 --warmup 2" ;;
-    em2) echo "--steps 10 --emulate 2 --emulate-rank 1" ;;
-    em4) echo "--steps 10 --emulate 4 --emulate-rank 3" ;;
-    em8) echo "--steps 10 --emulate 8 --emulate-rank 7" ;;
+    em2) echo "--steps 20 --warmup 5 --emulate 2 --emulate-rank 1" ;;
+    em4) echo "--steps 20 --warmup 5 --emulate 4 --emulate-rank 3" ;;
+    em8) echo "--steps 20 --warmup 5 --emulate 8 --emulate-rank 7" ;;
     c2) echo "--steps 10 --primary-only --spp-sqrt 1" ;;
     c3) echo "--steps 3 --scene $B/Antialiasing.json" ;;
     c4) echo "--steps 2 --scene $B/glossy_reflection.json --light-radius 1.0 --light-samples 4" ;;

@@ -13,7 +13,7 @@ B=tests/golden/scenes/blend
 args_for() {
   case "$1" in
     head) echo "--steps 10 --warmup 2" ;;
-    em8) echo "--steps 16 --warmup 8 --emulate 8 --emulate-rank 7" ;;
+    em8) echo "--steps 20 --warmup 5 --emulate 8 --emulate-rank 7" ;;
     c2) echo "--steps 10 --primary-only --spp-sqrt 1" ;;
     c3) echo "--steps 3 --scene $B/Antialiasing.json" ;;
     c4) echo "--steps 2 --scene $B/glossy_reflection.json --light-radius 1.0 --light-samples 4" ;;

@@ -10,14 +10,14 @@ source tools/gpu_steps.sh
 L=${1:?label}
 DEAL=${2:-lattice}
 SPLITS=${3:-2 4 8}
-STEPS=${4:-10}
+STEPS=${4:-20}
 D=gpurun_out/${L}_shares
 mkdir -p $D
-step ${L}_shares_head_whole.log 300 python3 bench.py --no-cpu-baseline --steps $STEPS ${BENCH_EXTRA:-}
+step ${L}_shares_head_whole.log 300 python3 bench.py --no-cpu-baseline --steps $STEPS --warmup 5 ${BENCH_EXTRA:-}
 cp gpurun_out/${L}_shares_head_whole.log $D/head_whole.log; grep "^{" $D/head_whole.log > $D/head_whole.json
 for N in $SPLITS; do
   for r in $(seq 0 $((N - 1))); do
-    step ${L}_shares_head_${N}_${r}.log 300 python3 bench.py --no-cpu-baseline --steps $STEPS --emulate $N --emulate-rank $r --deal $DEAL ${BENCH_EXTRA:-}
+    step ${L}_shares_head_${N}_${r}.log 300 python3 bench.py --no-cpu-baseline --steps $STEPS --warmup 5 --emulate $N --emulate-rank $r --deal $DEAL ${BENCH_EXTRA:-}
     grep "^{" gpurun_out/${L}_shares_head_${N}_${r}.log > $D/head_${N}_${r}.json
     echo "head $N-way rank $r $(python3 -c "import json;print(json.load(open('$D/head_${N}_${r}.json'))['value'])")"
   done
