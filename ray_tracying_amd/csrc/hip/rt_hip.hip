@@ -803,7 +803,8 @@ __device__ __forceinline__ float cull_limit(const TraceArgs& a, const Query& q, 
 // Issue priority around the node fetch (r06): a wave that has decided its next node runs at
 // s_setprio kVisitPrio until that node's loads are issued, then at 0 -- the SIMD's arbiter
 // prefers the waves about to fetch, so more fetches are in flight while the others compute
-// (same box, 3 reps: headline +1.1 % at 2, +1.3 % at 1; C3 +-0).  RT_SETPRIO=0 builds without.
+// (same box, 3 reps: headline +1.1 % at 2, +1.3 % at 1; C3 +-0; level 3 and the leaf phase at
+// priority 0 measured no better, profiles/r06l_ab_prio_variants.txt).  RT_SETPRIO=0 builds without.
 #ifndef RT_SETPRIO
 #define RT_SETPRIO 1
 #endif
