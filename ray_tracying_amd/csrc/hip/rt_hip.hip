@@ -902,6 +902,11 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   if (kCount) {
     const uint64_t wm = __ballot(1);
     if (a.diag && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 60, 1ull);  // wave-level node visits
+    if (a.diag) {  // ... of which every visiting lane's ray has the same direction octant
+      const uint64_t sx = __ballot(q.inv.x < 0.0f), sy = __ballot(q.inv.y < 0.0f), sz = __ballot(q.inv.z < 0.0f);
+      const bool uni = (sx == 0ull || sx == wm) && (sy == 0ull || sy == wm) && (sz == 0ull || sz == wm);
+      if (uni && __lane_id() == __ffsll((long long)wm) - 1) atomicAdd(a.counters + 57, 1ull);
+    }
     ++nvisit;
     const unsigned nb = __builtin_popcount((meta | (meta >> 1) | (meta >> 2) | (meta >> 3) | (meta >> 4) |
                                             (meta >> 5) | (meta >> 6) | (meta >> 7)) & 0x01010101u);
@@ -2749,6 +2754,29 @@ int rt_tile_costs(rt_scene_t s, const rt_camera_desc* cam, int32_t tile_w, int32
 
 }  // extern "C"
 
+// RT_DIAG on an instrumented (count_work) call, either path: shadow / other rays' box tests,
+// node and prim-test lane utilisation, and the wave node visits whose lanes share one
+// direction octant (control-block counters, trace_counters_out / node_visit)
+static int print_work_diag(const unsigned int* ctl) {
+  unsigned long long cnt[3] = {0, 0, 0};  // box tests, prim tests, rays (ctl bytes 16..)
+  HIP_TRY(hipMemcpy(cnt, ctl + 4, sizeof(cnt), hipMemcpyDeviceToHost), RT_EDEVICE);
+  unsigned long long dg[2] = {0, 0};
+  HIP_TRY(hipMemcpy(dg, ctl + 128, sizeof(dg), hipMemcpyDeviceToHost), RT_EDEVICE);
+  const unsigned long long cr = cnt[2] - dg[0], cb = cnt[0] - dg[1];
+  std::fprintf(stderr, "[rt diag] shadow rays %llu: %.1f box tests/ray; other rays %llu: %.1f box tests/ray\n", dg[0],
+               (double)dg[1] / (double)std::max(dg[0], 1ull), cr, (double)cb / (double)std::max(cr, 1ull));
+  unsigned long long wv[3] = {0, 0, 0};  // lane node visits, wave node visits, wave prim tests (ctl bytes 488..)
+  HIP_TRY(hipMemcpy(wv, ctl + 122, sizeof(wv), hipMemcpyDeviceToHost), RT_EDEVICE);
+  unsigned long long uo = 0;  // wave node visits with one direction octant (ctl byte 472)
+  HIP_TRY(hipMemcpy(&uo, ctl + 118, sizeof(uo), hipMemcpyDeviceToHost), RT_EDEVICE);
+  std::fprintf(stderr, "[rt diag] node visits: %.2f/ray, lane utilisation %.3f; prim tests: %.2f/ray, lane utilisation %.3f; "
+               "wave prim-test iterations per wave node visit %.2f; wave node visits with one octant %.3f\n",
+               (double)wv[0] / (double)std::max(cnt[2], 1ull), (double)wv[0] / (64.0 * (double)std::max(wv[1], 1ull)),
+               (double)cnt[1] / (double)std::max(cnt[2], 1ull), (double)cnt[1] / (64.0 * (double)std::max(wv[2], 1ull)),
+               (double)wv[2] / (double)std::max(wv[1], 1ull), (double)uo / (double)std::max(wv[1], 1ull));
+  return RT_OK;
+}
+
 // Finishes the scene's enqueued one-pass call: waits for its last event, records its measured
 // tile costs (instrumented calls) and fills `stats` (may be null).
 static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
@@ -2774,6 +2802,8 @@ static int finish_one_pass(rt_scene_s* s, rt_stats* stats) {
     diag_after_call(q.ta.counters, true);
   }
   s->last_iters = 1;
+  if (q.count_work && knob(K_DIAG, 0) != 0)
+    if (const int rc = print_work_diag((const unsigned int*)s->d_ctl)) return rc;
   if (!stats) return RT_OK;
   *stats = rt_stats{};
   const unsigned long long* h = s->h_stats;
@@ -3552,19 +3582,8 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     if (kDiagBuild) diag_after_call((const unsigned long long*)(ctl + 4), false);
     stats->node_visits = 0;
     if (p->count_work) stats->node_visits = h_stats[61];  // lane-level node visits (trace_counters_out, ctl byte 488)
-    if (p->count_work && knob(K_DIAG, 0) != 0) {
-      unsigned long long dg[2] = {0, 0};
-      HIP_TRY(hipMemcpy(dg, ctl + 128, sizeof(dg), hipMemcpyDeviceToHost), RT_EDEVICE);
-      const unsigned long long cr = cnt[2] - dg[0], cb = cnt[0] - dg[1];
-      std::fprintf(stderr, "[rt diag] shadow rays %llu: %.1f box tests/ray; other rays %llu: %.1f box tests/ray\n", dg[0],
-                   (double)dg[1] / (double)std::max(dg[0], 1ull), cr, (double)cb / (double)std::max(cr, 1ull));
-      unsigned long long wv[3] = {0, 0, 0};  // lane node visits, wave node visits, wave prim tests (ctl bytes 488..)
-      HIP_TRY(hipMemcpy(wv, ctl + 122, sizeof(wv), hipMemcpyDeviceToHost), RT_EDEVICE);
-      std::fprintf(stderr, "[rt diag] node visits: %.2f/ray, lane utilisation %.3f; prim tests: %.2f/ray, lane utilisation %.3f; wave prim-test iterations per wave node visit %.2f\n",
-                   (double)wv[0] / (double)std::max(cnt[2], 1ull), (double)wv[0] / (64.0 * (double)std::max(wv[1], 1ull)),
-                   (double)cnt[1] / (double)std::max(cnt[2], 1ull), (double)cnt[1] / (64.0 * (double)std::max(wv[2], 1ull)),
-                   (double)wv[2] / (double)std::max(wv[1], 1ull));
-    }
+    if (p->count_work && knob(K_DIAG, 0) != 0)
+      if (const int rc = print_work_diag(ctl)) return rc;
   }
   return RT_OK;
 }
