@@ -75,7 +75,10 @@ constexpr int kCtlBytes = 4096;    // control block (cleared by init_kernel)
 constexpr int kStatsBytes = 512;
 // scenes with fewer primitives spend their frame in the per-step passes over the slots, not in
 // traversal: their shadow rays are fused whatever the call size
-constexpr int kFuseFewPrims = 65536;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
+constexpr int kFuseFewPrims = 65536;
+// scenes of at most this many bounded primitives skip the traversal (TraceArgs::root_item;
+// RT_FLAT_PRIMS overrides, 0 = always traverse)
+constexpr int kFlatPrims = 8;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
 // Batch-claim counters of the logic step: one per 128-B line (kCtrStride words apart) --
 // atomics on one line serialise at the memory side, so the shards must not share lines.
 constexpr int kMaxBatchShards = 1024;
@@ -315,6 +318,12 @@ struct TraceArgs {
   const unsigned int* wave_done;  // per 64-slot group: all slots retired (nothing to fetch)
   int drain_help;             // once the queue is dry, free lanes search subtrees of busy lanes' queries
   int one_pass;               // one-pass call: every query is its unit's camera ray (camera_kernel), no slot state
+  // the first item of every traversal (render_tiles): the root node, kNoItem (linear mode, no
+  // bounded primitive) or -- -bvh on a scene of at most kFlatPrims bounded primitives -- one leaf
+  // item of all of them, so the leaf phase tests every bounded primitive, each candidate hit
+  // through the reference-leaf filter: the minimum the traversal finds (the tree prunes only
+  // subtrees that cannot hold a closer accepted hit), without the node visit and its stack
+  int root_item;
   int op_fo, op_ft, op_fk;    // one-pass query fields (LogicArgs): origin, time, kind; -1 absent
   // instrumented one-pass calls: node visits per render-order tile (unit / units per tile),
   // summed per wave at each work fetch -- the measured cost later calls of this camera order
@@ -1045,7 +1054,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
   const LaneStack S{reinterpret_cast<char*>(lds_stack), reinterpret_cast<int2*>(a.spill)};
   // the first item of every traversal (wave-uniform, in an SGPR of its own: as a VGPR constant
   // it was spilled and reloaded in the leaf loop)
-  const int root_item = sgpr_copy((a.c.n_prims > 0 && a.c.use_bvh && a.n_nodes > 0) ? 0 : kNoItem);
+  const int root_item = sgpr_copy(a.root_item);
   // a query was set up in q: start its traversal at the root (BVH::intersect_linear tests
   // every primitive at once, acceleration.cpp:124-139, and leaves nothing to traverse)
   auto start_traversal = [&]() {
@@ -3221,6 +3230,13 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   ta.drain_help = (int)knob(K_DRAIN_HELP, ta.drain_help);
   ta.lights = (const rt_light*)s->d_lights;
   ta.state = s->d_state;
+  {  // few-primitive scenes test every bounded primitive instead of traversing (r06: a root node
+     // and postponed leaves cost more than the few tests, and the lanes stay together)
+    const int n_bounded = s->desc.n_prims - s->desc.n_unbounded;
+    const bool flat = p->use_bvh && n_bounded > 0 && n_bounded <= std::min(127, (int)knob(K_FLAT_PRIMS, kFlatPrims));
+    ta.root_item = flat ? (int)(0x80000000u | (uint32_t)n_bounded)  // a leaf item: kLeafBit | first 0 << 7 | count
+                   : (s->desc.n_prims > 0 && p->use_bvh && s->desc.n_nodes > 0) ? 0 : -1;
+  }
   for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
   ta.light_samples = p->light_samples;
   // the closest hit starts its shade loop in the tracing lane too: planes, or untextured

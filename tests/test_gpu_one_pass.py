@@ -7,7 +7,8 @@ none, textures on planes only.  Each case renders through the default path (asse
 one-pass: rt_stats.path), through the step pipeline (RT_ONE_PASS=0) and as many one-pass tile
 chunks (RT_ONE_PASS_MAX), and every float must equal the oracle's (counter RNG) with equal
 ray counts.  The cases cover what the one-pass path branches on: planes with and without
-lights (plain / fused trace instances), the c3 == c2 unbounded list, textured planes (the
+lights (plain / fused trace instances; compact hits, r06, under a pinhole and a thin lens), the
+c3 == c2 unbounded list, textured planes (the
 hit's (u, v) from the trace kernel), transformed shapes with lights and without (the fused
 instance computing the hit record alone), a moving sphere (the ray time), a thin-lens
 camera (stored origins), tiles reaching past the image (the kind word), several lights.
@@ -65,7 +66,16 @@ def _multi_light_soup():
     return sc
 
 
+def _thin_lens_soup():
+    """A lit soup seen through a thin lens: the one-pass planes call's compact hits (r06) rebuild
+    each hit point from the stored lens origin (compact_hit's op_fo branch)."""
+    sc = scenes.soup(2500, seed=14, res=(56, 48))
+    sc["cameras"][0].update({"aperture": 0.3, "focus_dist": 4.0})
+    return sc
+
+
 CASES = {
+    "soup_thin_lens": (_thin_lens_soup, 2),
     "soup_lit": (lambda: scenes.soup(3000, seed=11, res=(96, 72)), 2),
     "soup_dark": (lambda: scenes.soup(3000, seed=12, res=(64, 64), light=False), 1),
     "soup_degenerate": (lambda: scenes.soup_degenerate(res=(48, 40)), 2),
