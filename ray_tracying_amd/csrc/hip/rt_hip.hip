@@ -3037,13 +3037,15 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   // 6263, 64M 6184, all 6319) or one rank's half of it (52M: 32M 5885, all 6225) -- else 128M
   // (C5 1.07G units: 96M 7666, 128M 7703, 192M 7705); scenes with reflection / refraction keep
   // 16M (C4: 8M 13043, 16M 13065, 32M 12791: their slots carry the Trace frames and take many
-  // short steps) -- since r05 6M in two slot pipelines (below).  ~180 B of HBM per slot: 128M
-  // slots ~23 GB.
+  // short steps) -- since r05 6M in two slot pipelines (below), since r06 8M (with the
+  // few-primitive leaf item a C4 trace launch is 15 % shorter and the pipelines want more slots
+  // per step: same box, 3 reps, 6M 15,829-15,836 Mrays/s, 7M 15,686-15,893, 8M 15,917-15,975,
+  // 10M 15,926-15,959, profiles/r06q_c4_slots.txt).  ~180 B of HBM per slot: 128M slots ~23 GB.
   const bool frames_scene = (s->desc.flags & (RT_SCENE_HAS_REFLECTION | RT_SCENE_HAS_REFRACTION)) != 0;
   const bool tex_scene = (s->desc.flags & RT_SCENE_HAS_TEXTURE) != 0;
   const bool one_pass = one_pass_scene(s) && one_pass_env() && n_units <= one_pass_cap();
   if (one_pass) note_ignored_knobs();
-  long long slots = frames_scene ? std::min(n_units, 6LL << 20) : std::min(n_units, 128LL << 20);
+  long long slots = frames_scene ? std::min(n_units, 8LL << 20) : std::min(n_units, 128LL << 20);
   slots = knob(K_SLOTS, slots);
   // slot-state words are addressed S[field * N + slot] in 32-bit int: (highest field + 1) * N
   // <= 2^31.  Scenes without Trace frames touch fields up to F_RAY + 2 (the ray origin), scenes

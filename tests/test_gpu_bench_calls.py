@@ -134,7 +134,7 @@ def test_c3_frame_as_timed(tmp_path, gpu):
 def test_c4_frame_as_timed(tmp_path, gpu):
     """C4 as timed: the whole glossy_reflection frame (light radius 1.0, -light_sample 4) on the
     step pipeline with its defaults for scenes with Trace frames -- two slot pipelines on two
-    streams, 6M slots between them, ~40 steps; tiles over the spheres, the cube and their
+    streams, 8M slots between them (r06), ~40 steps; tiles over the spheres, the cube and their
     reflections against the oracle."""
     src, path = _scene_as_bench_writes(tmp_path, "glossy_reflection", light_radius=1.0)
     img, line = _bench(tmp_path, "c4", "--scene", src, "--light-radius", "1.0", "--light-samples", "4")
