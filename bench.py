@@ -272,7 +272,8 @@ def parse():
     ap.add_argument("--frames-per-call", type=int, default=0,
                     help="frames rendered by one rt_render_frames call (one camera pass, one traversal launch, one "
                          "shading pass for all of them; one-pass scenes): 0 (auto) = the split N for a rank's share "
-                         "of an N-way split (so each call has the whole frame's samples), else 1")
+                         "of an N-way split (so each call has the whole frame's samples), frames of fewer than 4M "
+                         "samples as many as make 8M (at most 8: C2), else 1")
     ap.add_argument("--dump-frame", default=None,
                     help="after timing, render the frame at --seed with the timed steps' calls (same frames in "
                          "flight), gather it and save it (rank 0) as an (H, W, 3) .npy; unrendered tiles NaN")
@@ -538,8 +539,13 @@ def main():
     # frame is still rendered in full (its own seed) and gathered; the timed steps are the same K
     # frames.  Step-pipeline scenes render one frame per call.
     one_pass_path = cst.path == rt.PATH_ONE_PASS
+    # Small frames (C2: 1M samples, one short launch bound by its own tail) take the same route:
+    # as many frames per call as make 8M samples, at most 8 (r06, same box: C2 3,555 Mrays/s with
+    # three frames in flight, 4,479 / 5,355 / 5,761 at 4 / 8 / 16 frames per call,
+    # profiles/r06t_c2_frames_per_call.txt)
     B = args.frames_per_call if args.frames_per_call > 0 else (
-        max(1, min(split, (2 ** 30) // max(units, 1))) if one_pass_path and split > 1 else 1)
+        max(1, min(split, (2 ** 30) // max(units, 1))) if one_pass_path and split > 1 else
+        max(1, min(8, -(-(8 * 2 ** 20) // max(units, 1)))) if one_pass_path and units < 4 * 2 ** 20 else 1)
     if not one_pass_path:
         B = 1
     if B > 1:

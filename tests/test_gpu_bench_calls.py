@@ -93,6 +93,29 @@ def test_rank_share_as_timed(soup1024, tmp_path, gpu):
     assert rays == line["config"]["rays_per_step"]
 
 
+def test_c2_frame_as_timed(tmp_path_factory, tmp_path, gpu):
+    """C2 as timed (r06): the 1024^2 x 1 spp primary-only soup frame rendered eight frames per
+    rt_render_frames call (small frames: as many as make 8M samples), the frame at --seed the last
+    of them; the whole frame against the oracle with an equal ray count."""
+    path = str(tmp_path_factory.mktemp("soupc2") / "soup1m.json")
+    rt.make_soup(path, 1_000_000, seed=SEED, width=1024, height=1024)
+    txt = open(path).read()  # the soup with "lights": [] as bench.py writes it for --primary-only
+    i = txt.index('"lights": [')
+    j = txt.index("\n", i)
+    open(path, "w").write(txt[:i] + '"lights": [],' + txt[j:])
+    img, line = _bench(tmp_path, "c2", "--primary-only", "--spp-sqrt", "1")
+    assert line["config"]["frames_per_call"] == 8 and line["config"]["pipeline"].startswith("one-pass")
+    assert np.isfinite(img).all()
+    tiles_x = 1024 // T
+    regions = [((t % tiles_x) * T, (t // tiles_x) * T, T, T) for t in range(256)]
+    ref, ost = ob.render_regions(path, regions, use_bvh=True, spp_sqrt=1, light_samples=1, seed=SEED,
+                                 resolution=(1024, 1024))
+    for k, (x0, y0, _, _) in enumerate(regions):
+        got = np.ascontiguousarray(img[y0:y0 + T, x0:x0 + T])
+        assert int((got.view(np.uint32) != ref[k].view(np.uint32)).sum()) == 0, f"tile {k}"
+    assert ost["rays"] == line["config"]["rays_per_step"]
+
+
 def test_c5_frame_as_timed(tmp_path_factory, tmp_path, gpu):
     """C5 as timed: the whole 4096^2 x 64 spp frame (2^30 units) in one one-pass call; tiles at
     the centre, the corners, the edges and across the soup's silhouette (64 x 64 tile grid)."""
