@@ -82,6 +82,37 @@ def valu_block(pv: dict, pmc_valu: str, peak_ipc: float, peak_src: str) -> dict:
             "source": f"{os.path.relpath(pmc_valu, ROOT)} ({pv.get('label', '')})"}
 
 
+def frames_per_call(requested: int, one_pass: bool, split: int, units: int) -> int:
+    """Frames per rt_render_frames call (--frames-per-call; 0 = auto).  Auto: a rank's share of an
+    N-way split renders N frames per call (each call the whole frame's size, at most 2^30
+    samples); a frame of fewer than 4M samples as many as make 8M (at most 8: C2); else 1.  The
+    step pipeline renders one frame per call (rt_render_frames would run them one after another)."""
+    if not one_pass:
+        return 1
+    if requested > 0:
+        return requested
+    if split > 1:
+        return max(1, min(split, (2 ** 30) // max(units, 1)))
+    if units < 4 * 2 ** 20:
+        return max(1, min(8, -(-(8 * 2 ** 20) // max(units, 1))))
+    return 1
+
+
+def frame_groups(seeds, b: int):
+    """The frames split into calls of at most b, as evenly as possible (20 frames, b = 8:
+    7 + 7 + 6), so that no call is much smaller than the others."""
+    n = len(seeds)
+    if n == 0:
+        return []
+    k = -(-n // b)
+    sizes = [n // k + (1 if i < n % k else 0) for i in range(k)]
+    out, i = [], 0
+    for sz in sizes:
+        out.append(list(seeds[i:i + sz]))
+        i += sz
+    return out
+
+
 def cpu_baseline_rank(args) -> int | None:
     """The rank that times the reference CPU path after the timed steps: rank 0 at every N (the
     north_star asks for it beside the 1, 2, 4 and 8-GPU numbers), none with --no-cpu-baseline."""
@@ -543,11 +574,7 @@ def main():
     # as many frames per call as make 8M samples, at most 8 (r06, same box: C2 3,555 Mrays/s with
     # three frames in flight, 4,479 / 5,355 / 5,761 at 4 / 8 / 16 frames per call,
     # profiles/r06t_c2_frames_per_call.txt)
-    B = args.frames_per_call if args.frames_per_call > 0 else (
-        max(1, min(split, (2 ** 30) // max(units, 1))) if one_pass_path and split > 1 else
-        max(1, min(8, -(-(8 * 2 ** 20) // max(units, 1)))) if one_pass_path and units < 4 * 2 ** 20 else 1)
-    if not one_pass_path:
-        B = 1
+    B = frames_per_call(args.frames_per_call, one_pass_path, split, units)
     if B > 1:
         out = torch.zeros(B * out.numel(), dtype=torch.float32, device=f"cuda:{dev}")
     share_floats = out.numel() // B  # per frame, padded to the largest rank's share (equal gathers)
@@ -564,25 +591,11 @@ def main():
     fl_st = [torch.cuda.Stream(device=dev) for _ in range(F)] if F > 1 else []
     last_group = [1]  # frames in the last call's buffer (the last gathered frame is its last)
 
-    def groups(seeds):
-        """The frames split into calls of at most B, as evenly as possible (20 frames, B = 8:
-        7 + 7 + 6), so that no call is much smaller than the others."""
-        n = len(seeds)
-        if n == 0:
-            return []
-        k = -(-n // B)
-        sizes = [n // k + (1 if i < n % k else 0) for i in range(k)]
-        out_g, i = [], 0
-        for sz in sizes:
-            out_g.append(seeds[i:i + sz])
-            i += sz
-        return out_g
-
     def multi(seeds):
         """B > 1: each group of frames is one rt_render_frames call into `out` (frame-major), then
         one gather of the group's frames."""
         sts = []
-        for g in groups(seeds):
+        for g in frame_groups(seeds, B):
             params.seed = g[0]
             st = ds.render_frames(g, mine, T, T, out.data_ptr(), params)
             last_group[0] = len(g)

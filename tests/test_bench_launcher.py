@@ -80,3 +80,29 @@ def test_world_size_mismatch_fails():
     r = _run(["--gpus", "8", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "WORLD_SIZE=1" in r.stderr and r.stdout.strip() == ""
+
+
+def test_frames_per_call_rule():
+    """bench.py's frames per rt_render_frames call (r06): a rank's share of an N-way split renders
+    N frames per call (the whole frame's size), small frames (C2: 1M samples) eight, whole frames
+    and the step pipeline one; --frames-per-call overrides for one-pass scenes only."""
+    M = 2 ** 20
+    assert bench.frames_per_call(0, True, 8, 13 * M) == 8
+    assert bench.frames_per_call(0, True, 4, 26 * M) == 4
+    assert bench.frames_per_call(0, True, 8, 134 * M) == 7  # C5's eighth: 2^30 samples at most
+    assert bench.frames_per_call(0, True, 1, 1 * M) == 8
+    assert bench.frames_per_call(0, True, 1, 3 * M) == 3
+    assert bench.frames_per_call(0, True, 1, 100 * M) == 1
+    assert bench.frames_per_call(0, False, 8, 13 * M) == 1
+    assert bench.frames_per_call(5, True, 1, 100 * M) == 5
+    assert bench.frames_per_call(5, False, 1, 100 * M) == 1
+
+
+@pytest.mark.parametrize("n,b", [(20, 8), (20, 7), (5, 8), (1, 8), (16, 8), (30, 8), (0, 3)])
+def test_frame_groups(n, b):
+    seeds = list(range(100, 100 + n))
+    g = bench.frame_groups(seeds, b)
+    assert [x for grp in g for x in grp] == seeds  # every frame once, in order
+    assert all(1 <= len(grp) <= b for grp in g)
+    if g:
+        assert max(map(len, g)) - min(map(len, g)) <= 1 and len(g) == -(-n // b)
