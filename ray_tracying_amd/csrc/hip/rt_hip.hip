@@ -122,8 +122,11 @@ struct HitRec {
   uint32_t mat;
 };
 __device__ __forceinline__ float* hit_rec(float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
-// TraceArgs::has_tex: what a closest hit leaves for the shading (finish_query)
-constexpr int kHitRecord = 0, kHitTex = 1, kHitCompact = 2;
+// TraceArgs::has_tex: what a closest hit leaves for the shading (finish_query / settle):
+// the 32-B record, the record and (u, v), the hit's t alone (one-pass planes calls), or
+// nothing beyond the result index (kHitRecompute: one-pass calls of transformed shapes, whose
+// shading recomputes the hit -- compact_hit)
+constexpr int kHitRecord = 0, kHitTex = 1, kHitCompact = 2, kHitRecompute = 3;
 __device__ __forceinline__ const float* hit_rec(const float* hit, int slot) { return hit + (size_t)slot * HIT_STRIDE; }
 __device__ __forceinline__ const float* hit_rec_u(const float* hit, size_t unit) { return hit + unit * HIT_STRIDE; }
 // point + normal + material
@@ -297,7 +300,8 @@ struct TraceArgs {
   float* hit;                 // [n_slots][HIT_STRIDE]: attributes of a closest hit (for the logic step)
   float2* hit_uv;             // [n_slots]: (u, v) of a closest hit, textured scenes
   int has_tex;                // hit output: kHitRecord (32-B record), kHitTex (some material is textured:
-                              // the record and (u, v)), kHitCompact (one-pass planes calls: t alone)
+                              // the record and (u, v)), kHitCompact (one-pass planes calls: t alone),
+                              // kHitRecompute (one-pass transformed-shape calls: nothing)
   int refill_min;             // refill kernel: refill finished lanes when fewer than this many traverse
   int leaf_min;               // refill kernel: test postponed leaves once this many lanes wait on one
   int diag;                   // count_work under RT_DIAG: wave-level utilisation counters
@@ -1178,7 +1182,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RT_INSTA
           HitAttr at;
           float t;
           prim_hit<true, false, false>(P, rec, q.r, t, &at);
-          store_hit_pnm(hit_rec(a.hit, slot), at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
+          if (a.has_tex != kHitRecompute) store_hit_pnm(hit_rec(a.hit, slot), at.p, at.n, RT_TAG_MATERIAL(prim_tag(P)));
           hp = at.p;
           hn = at.n;
           have = true;
@@ -2105,7 +2109,10 @@ __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit, i
 #ifndef RT_SR_WAVES
 #define RT_SR_WAVES 6
 #endif
-constexpr int kSrPixels = RT_SR_PIXELS, kSrChunk = 8, kSrStride = kSrChunk * 3 + 1;  // odd row: conflict-free sums
+#ifndef RT_SR_CHUNK
+#define RT_SR_CHUNK 8
+#endif
+constexpr int kSrPixels = RT_SR_PIXELS, kSrChunk = RT_SR_CHUNK, kSrStride = kSrChunk * 3 + 1;  // odd row: conflict-free sums
 constexpr int kSrUnits = kSrPixels * kSrChunk / kBlock;                     // units per thread per pass
 // kHitCompact calls (r06): the hit record finish_query used to store, rebuilt here from what the
 // trace kernel keeps -- the hit's t -- and what the call already holds: the unit's camera ray
@@ -2124,7 +2131,28 @@ __device__ __forceinline__ HitRec compact_hit(const LogicArgs& a, size_t unit, i
   const V3 d{a.query[unit], a.query[N + unit], a.query[2 * N + unit]};
   return HitRec{V3{o.x + t * d.x, o.y + t * d.y, o.z + t * d.z}, V3{ns.x, ns.y, ns.z}, 0.0f, 0.0f, __float_as_uint(ns.w)};
 }
-template <bool kTex, bool kCompact>
+// kHitRecompute calls (r06, transformed shapes): the record the trace kernel's settle computed
+// for its fused shadow ray and no longer stores -- prim_hit with attributes on the same
+// primitive and the same ray (the unit's camera ray and its time), so the same bits.
+__device__ __forceinline__ HitRec recompute_hit(const LogicArgs& a, size_t unit, int res) {
+  const size_t N = (size_t)(unsigned)a.n_slots;
+  Ray r;
+  r.o = V3{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
+  if (a.op_fo >= 0) {
+    const float* Qo = a.query + (size_t)a.op_fo * N + unit;
+    r.o = V3{Qo[0], Qo[N], Qo[2 * N]};
+  }
+  r.d = V3{a.query[unit], a.query[N + unit], a.query[2 * N + unit]};
+  r.time = a.op_ft >= 0 ? a.query[(size_t)a.op_ft * N + unit] : 0.0f;
+  const float4* rec = a.c.prims + (size_t)res * a.c.prim_stride4;
+  PrimA P;
+  load_prim_a(rec, P);
+  HitAttr at;
+  float t;
+  prim_hit<true, false, false>(P, rec, r, t, &at);
+  return HitRec{at.p, at.n, 0.0f, 0.0f, RT_TAG_MATERIAL(prim_tag(P))};
+}
+template <bool kTex, int kHit>
 __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(LogicArgs a) {
   __shared__ float stage[kSrPixels * kSrStride];
   const int p0 = blockIdx.x * kSrPixels;
@@ -2148,7 +2176,8 @@ __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(Logic
     HitRec hr[kSrUnits];
 #pragma unroll
     for (int m = 0; m < kSrUnits; ++m) {
-      if constexpr (kCompact) hr[m] = res[m] >= 0 ? compact_hit(a, u[m], res[m]) : HitRec{};
+      if constexpr (kHit == kHitCompact) hr[m] = res[m] >= 0 ? compact_hit(a, u[m], res[m]) : HitRec{};
+      else if constexpr (kHit == kHitRecompute) hr[m] = res[m] >= 0 ? recompute_hit(a, u[m], res[m]) : HitRec{};
       else hr[m] = res[m] >= 0 ? load_hit(hit_rec_u(a.hit, u[m])) : HitRec{};
     }
 #pragma unroll
@@ -3308,11 +3337,13 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
                  fixed ? "constant loop parameters" : "runtime loop parameters");
   ta.occl = s->d_occl;
   la.n_fuse = ta.n_fuse;
-  // one-pass planes-only calls without textures and with at most one fused light keep only the
-  // hit's t (kHitCompact; a later light's shadow ray would reload the full record); RT_COMPACT_HIT=0
-  // keeps the 32-B record
-  if (one_pass && planes_only && ta.has_tex == kHitRecord && ta.n_fuse <= 1 && knob(K_COMPACT_HIT, 1) != 0)
-    ta.has_tex = kHitCompact;
+  // one-pass calls without textures and with at most one fused light (a later light's shadow ray
+  // would reload the full record) store no 32-B hit record: planes-only calls keep the hit's t
+  // (kHitCompact), calls of transformed shapes nothing (kHitRecompute: the shading recomputes the
+  // hit, r06 A/B same box: C3 +6.2 %, the trace launch -15 %; headline +-0); RT_COMPACT_HIT=0
+  // keeps the record
+  if (one_pass && ta.has_tex == kHitRecord && ta.n_fuse <= 1 && knob(K_COMPACT_HIT, 1) != 0)
+    ta.has_tex = planes_only ? kHitCompact : kHitRecompute;
   la.occl = s->d_occl;
   ta.counters = (unsigned long long*)(ctl + 4);  // byte 16
   // entry + t_near per stack slot
@@ -3466,10 +3497,12 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
     const unsigned rblocks = (unsigned)((n_pixels + kSrPixels - 1) / kSrPixels);
-    if (tex) hipLaunchKernelGGL((shade_reduce_kernel<true, false>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+    if (tex) hipLaunchKernelGGL((shade_reduce_kernel<true, kHitRecord>), dim3(rblocks), dim3(kBlock), 0, stream, la);
     else if (ta.has_tex == kHitCompact)
-      hipLaunchKernelGGL((shade_reduce_kernel<false, true>), dim3(rblocks), dim3(kBlock), 0, stream, la);
-    else hipLaunchKernelGGL((shade_reduce_kernel<false, false>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+      hipLaunchKernelGGL((shade_reduce_kernel<false, kHitCompact>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+    else if (ta.has_tex == kHitRecompute)
+      hipLaunchKernelGGL((shade_reduce_kernel<false, kHitRecompute>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+    else hipLaunchKernelGGL((shade_reduce_kernel<false, kHitRecord>), dim3(rblocks), dim3(kBlock), 0, stream, la);
     HIP_TRY(hipGetLastError(), RT_EDEVICE);
     HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     if (measure_tiles)
