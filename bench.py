@@ -83,19 +83,21 @@ def valu_block(pv: dict, pmc_valu: str, peak_ipc: float, peak_src: str) -> dict:
 
 
 def frames_per_call(requested: int, one_pass: bool, split: int, units: int) -> int:
-    """Frames per rt_render_frames call (--frames-per-call; 0 = auto).  Auto: a rank's share of an
-    N-way split renders N frames per call (each call the whole frame's size, at most 2^30
-    samples); a frame of fewer than 4M samples as many as make 8M (at most 8: C2); else 1.  The
-    step pipeline renders one frame per call (rt_render_frames would run them one after another)."""
+    """Frames per rt_render_frames call (--frames-per-call; 0 = auto).  Auto: up to eight whole
+    frames' samples per call -- 8 frames of a whole frame, 8N of a rank's share of an N-way split,
+    so a share's launch has the whole-frame run's size -- and at most 2^30 samples (C5: 1); a frame
+    of fewer than 4M samples (C2) as many as make 64M (at most 64).  One traversal launch per call:
+    its tail, and the camera and shading launches, are paid once per call (r06 sweep, same box:
+    headline 1 / 4 / 8 frames 8,322-8,374 / 8,535-8,567 / 8,566-8,576 Mrays/s, C3 +3 % at 8, C2
+    5,494 / 6,516-6,583 at 8 / 64; profiles/r06ad_frames_per_call_sweep.txt).  The step pipeline
+    renders one frame per call (rt_render_frames would run them one after another)."""
     if not one_pass:
         return 1
     if requested > 0:
         return requested
-    if split > 1:
-        return max(1, min(split, (2 ** 30) // max(units, 1)))
-    if units < 4 * 2 ** 20:
-        return max(1, min(8, -(-(8 * 2 ** 20) // max(units, 1))))
-    return 1
+    if split <= 1 and units < 4 * 2 ** 20:
+        return max(1, min(64, -(-(64 * 2 ** 20) // max(units, 1))))
+    return max(1, min(8 * max(split, 1), (2 ** 30) // max(units, 1)))
 
 
 def frame_groups(seeds, b: int):
@@ -561,19 +563,17 @@ def main():
     # rays and this frame's shading run in the idle tail of the other frame's trace launch.
     # Every frame is rendered in full and gathered; steps are timed exactly as with F = 1.
     units = len(mine) * T * T * max(1, args.spp_sqrt) ** 2
-    # Frames per call (r06): a rank's share of a split frame renders B consecutive frames in ONE
-    # rt_render_frames call -- every sample of them in one camera pass, one traversal launch and
-    # one shading pass -- so its launches have the whole frame's size (B = the split: 8 frames of
-    # an eighth = 105M samples) and run what a whole frame runs (the 7-wave traversal, one short
-    # tail per B frames) instead of a launch an eighth that size, whose drain and missing seventh
-    # wave held one rank's eighth at 0.84 of the whole frame's rate (r05).  Every
-    # frame is still rendered in full (its own seed) and gathered; the timed steps are the same K
-    # frames.  Step-pipeline scenes render one frame per call.
+    # Frames per call (r06): B consecutive frames render in ONE rt_render_frames call -- every
+    # sample of them in one camera pass, one traversal launch and one shading pass -- so a
+    # launch's drain tail and the short camera / shading launches are paid once per B frames.
+    # Auto (frames_per_call): up to eight whole frames' samples per call, so a rank's share of an
+    # N-way split renders 8N frames per call and its launches have the whole-frame run's size (the
+    # 7-wave traversal, the same tail share) -- r05's eighth, one launch an eighth the size, ran at
+    # 0.84 of the whole frame's rate; small frames (C2: 1M samples, one short launch
+    # bound by its own tail) as many as make 64M.  Every frame is still rendered in full (its own
+    # seed) and gathered; the timed steps are the same K frames (profiles/r06ad_frames_per_call_sweep.txt,
+    # r06t_c2_frames_per_call.txt).  Step-pipeline scenes render one frame per call.
     one_pass_path = cst.path == rt.PATH_ONE_PASS
-    # Small frames (C2: 1M samples, one short launch bound by its own tail) take the same route:
-    # as many frames per call as make 8M samples, at most 8 (r06, same box: C2 3,555 Mrays/s with
-    # three frames in flight, 4,479 / 5,355 / 5,761 at 4 / 8 / 16 frames per call,
-    # profiles/r06t_c2_frames_per_call.txt)
     B = frames_per_call(args.frames_per_call, one_pass_path, split, units)
     if B > 1:
         out = torch.zeros(B * out.numel(), dtype=torch.float32, device=f"cuda:{dev}")
@@ -740,10 +740,15 @@ def main():
     pmc_traffic = args.pmc_traffic or (prof + "_pmc_traffic.json" if headline or c5 else None)
     pmc_valu = args.pmc_valu or (prof + "_pmc_valu.json" if headline or c5 else None)
     traffic, traffic_src, pv = None, None, None
+    frames_per_launch = args.steps * world / launches_all if launches_all else 1.0
     if pmc_traffic and os.path.exists(pmc_traffic):
         pm = json.load(open(pmc_traffic))
-        traffic = pm.get("hbm_bytes_per_launch")
-        traffic_src = f"{os.path.relpath(pmc_traffic, ROOT)} ({pm.get('label', '')})"
+        # per frame (the profiled launches' frame count: tools/pmc_traffic.py --frames), then per
+        # launch of this run
+        per_frame = pm.get("hbm_bytes_per_frame", pm.get("hbm_bytes_per_launch", 0) / pm.get("frames_per_launch", 1))
+        traffic = round(per_frame * frames_per_launch) if per_frame else None
+        traffic_src = (f"{os.path.relpath(pmc_traffic, ROOT)} ({pm.get('label', '')}; "
+                       f"{pm.get('frames_per_launch', 1)} frame(s) per profiled launch)")
     if pmc_valu and os.path.exists(pmc_valu):
         pv = json.load(open(pmc_valu))
     kernel = {
@@ -774,6 +779,7 @@ def main():
             "achieved": valu["achieved"] if valu else None, "peak": round(spec_tops, 2),
             "unit": "T VALU lane-ops/s", "frac": valu["frac"] if valu else None,
             "traffic": traffic, "traffic_unit": "HBM bytes per trace launch (PMC)", "traffic_source": traffic_src,
+            "traffic_per_frame": round(traffic / frames_per_launch) if traffic else None,
             "peak_definition": "the guide's VALU peak (MI355X_MICROARCH.md: a wave64 instruction issues over 2 "
                                "cycles on each of 4 SIMD-32 per CU = 2 wave64 instructions per CU-cycle) x 256 CUs x "
                                "64 lanes x 2.4 GHz; achieved = PMC wave64 VALU instructions/s x 64 x lane utilisation; "

@@ -83,16 +83,19 @@ def test_world_size_mismatch_fails():
 
 
 def test_frames_per_call_rule():
-    """bench.py's frames per rt_render_frames call (r06): a rank's share of an N-way split renders
-    N frames per call (the whole frame's size), small frames (C2: 1M samples) eight, whole frames
-    and the step pipeline one; --frames-per-call overrides for one-pass scenes only."""
+    """bench.py's frames per rt_render_frames call (r06): up to eight whole frames' samples per
+    call -- 8 frames of a whole frame, 8N of a rank's share of an N-way split -- at most 2^30
+    samples; small frames (C2: 1M samples) as many as make 64M; the step pipeline one;
+    --frames-per-call overrides for one-pass scenes only."""
     M = 2 ** 20
-    assert bench.frames_per_call(0, True, 8, 13 * M) == 8
-    assert bench.frames_per_call(0, True, 4, 26 * M) == 4
+    assert bench.frames_per_call(0, True, 1, 100 * M) == 8  # the headline frame (104.9M samples)
+    assert bench.frames_per_call(0, True, 8, 13 * M) == 64  # a rank's eighth: 8 whole frames' samples
+    assert bench.frames_per_call(0, True, 4, 26 * M) == 32
+    assert bench.frames_per_call(0, True, 2, 52 * M) == 16
     assert bench.frames_per_call(0, True, 8, 134 * M) == 7  # C5's eighth: 2^30 samples at most
-    assert bench.frames_per_call(0, True, 1, 1 * M) == 8
-    assert bench.frames_per_call(0, True, 1, 3 * M) == 3
-    assert bench.frames_per_call(0, True, 1, 100 * M) == 1
+    assert bench.frames_per_call(0, True, 1, 1024 * M) == 1  # C5's whole frame
+    assert bench.frames_per_call(0, True, 1, 1 * M) == 64  # C2
+    assert bench.frames_per_call(0, True, 1, 3 * M) == 22
     assert bench.frames_per_call(0, False, 8, 13 * M) == 1
     assert bench.frames_per_call(5, True, 1, 100 * M) == 5
     assert bench.frames_per_call(5, False, 1, 100 * M) == 1

@@ -70,9 +70,12 @@ def _compare(img, path, res, spp_sqrt, tiles):
 
 
 def test_headline_frame_as_timed(soup1024, tmp_path, gpu):
-    """bench.py's default step: the whole 1024^2 x 100 spp frame in one one-pass call."""
+    """bench.py's default step: the whole 1024^2 x 100 spp frame, rendered as the last of eight
+    frames of one rt_render_frames call (r06: one camera pass, one traversal launch, one shading
+    pass for the eight)."""
     img, line = _bench(tmp_path, "head")
     assert line["config"]["frames_in_flight"] == 1 and line["config"]["pipeline"].startswith("one-pass")
+    assert line["config"]["frames_per_call"] == 8
     assert np.isfinite(img).all()
     rays = _compare(img, soup1024, 1024, 10, list(range(16 * 16)))
     assert rays == line["config"]["rays_per_step"]
@@ -80,10 +83,11 @@ def test_headline_frame_as_timed(soup1024, tmp_path, gpu):
 
 def test_rank_share_as_timed(soup1024, tmp_path, gpu):
     """One rank's share of the 8-way split (rank 7: 32 tiles of the lattice deal) rendered as its
-    rank does (r06): eight frames per rt_render_frames call -- one camera pass, one traversal
-    launch of the whole frame's size, one shading pass -- the frame at --seed the last of them."""
+    rank does (r06): 64 frames per rt_render_frames call -- one camera pass, one traversal
+    launch of the whole-frame run's size (eight whole frames' samples), one shading pass -- the
+    frame at --seed the last of them."""
     img, line = _bench(tmp_path, "em8", "--emulate", "8", "--emulate-rank", "7")
-    assert line["config"]["frames_per_call"] == 8 and line["config"]["frames_in_flight"] == 1
+    assert line["config"]["frames_per_call"] == 64 and line["config"]["frames_in_flight"] == 1
     mine = [int(t) for t in tl.assign_tiles(256, 8, 7, 16)]
     assert len(mine) == 32
     done = np.isfinite(img).all(axis=2)
@@ -94,8 +98,8 @@ def test_rank_share_as_timed(soup1024, tmp_path, gpu):
 
 
 def test_c2_frame_as_timed(tmp_path_factory, tmp_path, gpu):
-    """C2 as timed (r06): the 1024^2 x 1 spp primary-only soup frame rendered eight frames per
-    rt_render_frames call (small frames: as many as make 8M samples), the frame at --seed the last
+    """C2 as timed (r06): the 1024^2 x 1 spp primary-only soup frame rendered 64 frames per
+    rt_render_frames call (small frames: as many as make 64M samples), the frame at --seed the last
     of them; the whole frame against the oracle with an equal ray count."""
     path = str(tmp_path_factory.mktemp("soupc2") / "soup1m.json")
     rt.make_soup(path, 1_000_000, seed=SEED, width=1024, height=1024)
@@ -104,7 +108,7 @@ def test_c2_frame_as_timed(tmp_path_factory, tmp_path, gpu):
     j = txt.index("\n", i)
     open(path, "w").write(txt[:i] + '"lights": [],' + txt[j:])
     img, line = _bench(tmp_path, "c2", "--primary-only", "--spp-sqrt", "1")
-    assert line["config"]["frames_per_call"] == 8 and line["config"]["pipeline"].startswith("one-pass")
+    assert line["config"]["frames_per_call"] == 64 and line["config"]["pipeline"].startswith("one-pass")
     assert np.isfinite(img).all()
     tiles_x = 1024 // T
     regions = [((t % tiles_x) * T, (t // tiles_x) * T, T, T) for t in range(256)]
@@ -144,12 +148,14 @@ def _scene_as_bench_writes(tmp_path, name, light_radius=None):
 
 
 def test_c3_frame_as_timed(tmp_path, gpu):
-    """C3 as timed: the whole Antialiasing frame (1024^2 x 100 spp) in one one-pass call over all
-    256 tiles (transformed shapes: byte-code nodes, fused point-light shadows in the tracing
-    lane); the cube's faces and silhouette and the lit floor against the oracle."""
+    """C3 as timed: the whole Antialiasing frame (1024^2 x 100 spp) as the last of eight frames of
+    one one-pass rt_render_frames call over all 256 tiles (transformed shapes: byte-code nodes,
+    fused point-light shadows in the tracing lane, the hit recomputed by the shading); the cube's
+    faces and silhouette and the lit floor against the oracle."""
     src, path = _scene_as_bench_writes(tmp_path, "Antialiasing")
     img, line = _bench(tmp_path, "c3", "--scene", src)
     assert line["config"]["pipeline"].startswith("one-pass") and line["config"]["frames_in_flight"] == 1
+    assert line["config"]["frames_per_call"] == 8
     assert np.isfinite(img).all()
     _compare(img, path, 1024, 10, [9 * 16 + 7, 12 * 16 + 6, 7 * 16 + 6, 3 * 16 + 12, 0, 255])
 

@@ -46,6 +46,9 @@ def main() -> None:
     ap.add_argument("--kernel", default=r"trace_(refill_)?kernel(ILb0E|<false)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--label", default="")
+    # frames per traversal launch in the profiled run (bench.py --frames-per-call / its auto rule;
+    # every profiled launch must render the same count): per-frame bytes for the bench line
+    ap.add_argument("--frames", type=int, default=1)
     a = ap.parse_args()
     fe = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     wr = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
@@ -65,6 +68,9 @@ def main() -> None:
         "fetch_bytes_per_launch_corrected": round(fetch_b),
         "write_bytes_per_launch": round(write_b),
         "hbm_bytes_per_launch": round(fetch_b + write_b),
+        "frames_per_launch": a.frames,
+        "hbm_bytes_per_frame": round((fetch_b + write_b) / max(1, a.frames)),
+        "write_bytes_per_frame": round(write_b / max(1, a.frames)),
         "correction": "FETCH_SIZE x2 (gfx950 tallies 128-B read requests at 64 B); WRITE_SIZE as is",
     }
     with open(a.out, "w") as fh:
