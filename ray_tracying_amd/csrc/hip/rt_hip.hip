@@ -843,11 +843,14 @@ __device__ __forceinline__ int node_visit(const TraceArgs& a, const Query& q, fl
   float tnx[4], tfx[4], tny[4], tfy[4], tnz[4], tfz[4];
   int cc[4];
   uint32_t meta;  // count_work: byte k nonzero for a child in slot k
+  // the slab terms of the node's grid: plane = origin + code * 2^k per axis, so t = A + code * B
+  // with A = (origin - o) * inv and B = inv * 2^k -- one v_ldexp_f32 from the node's signed
+  // exponent byte k (upload_nodes), the bits the multiply by the power-of-two float gives
   auto g_terms = [&](const float4 g, float& ax, float& bx, float& ay, float& by, float& az, float& bz) {
-    const uint32_t ex = __float_as_uint(g.w);
-    ax = (g.x - r.o.x) * inv.x, bx = __uint_as_float((ex & 0xffu) << 23) * inv.x;
-    ay = (g.y - r.o.y) * inv.y, by = __uint_as_float(((ex >> 8) & 0xffu) << 23) * inv.y;
-    az = (g.z - r.o.z) * inv.z, bz = __uint_as_float(((ex >> 16) & 0xffu) << 23) * inv.z;
+    const int ex = __float_as_int(g.w);
+    ax = (g.x - r.o.x) * inv.x, bx = __builtin_ldexpf(inv.x, (ex << 24) >> 24);
+    ay = (g.y - r.o.y) * inv.y, by = __builtin_ldexpf(inv.y, (ex << 16) >> 24);
+    az = (g.z - r.o.z) * inv.z, bz = __builtin_ldexpf(inv.z, (ex << 8) >> 24);
   };
   float ax, bx, ay, by, az, bz;
   if constexpr (kF16) {
@@ -2545,8 +2548,19 @@ static uint32_t f16_code(uint32_t c) {  // binary16 bits of the integer c < 2048
   int e = 31 - __builtin_clz(c);
   return (uint32_t)(e + 15) << 10 | ((c << (10 - e)) & 0x3ffu);
 }
+// the grid steps' exponent bytes unbiased: int8 k = e - 127 (bvh_wide: e in [1, 207]), the
+// device nodes' form (node_visit's v_ldexp_f32 takes k as it is; r06)
+static uint32_t signed_exps(uint32_t exps) {
+  uint32_t ks = 0;
+  for (int a = 0; a < 3; ++a) ks |= (uint32_t)(uint8_t)(int8_t)((int)((exps >> (8 * a)) & 0xffu) - 127) << (8 * a);
+  return ks;
+}
 static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n, bool planes_only) {
-  if (!planes_only) return upload(dst, nodes, (size_t)n * sizeof(rt_node4));
+  if (!planes_only) {
+    std::vector<rt_node4> v(nodes, nodes + n);
+    for (rt_node4& d : v) d.exps = signed_exps(d.exps);
+    return upload(dst, v.data(), v.size() * sizeof(rt_node4));
+  }
   std::vector<NodeF16> v((size_t)n);
   for (int32_t i = 0; i < n; ++i) {
     const rt_node4& s = nodes[i];
@@ -2558,7 +2572,7 @@ static int upload_nodes(void** dst, const rt_node4* nodes, int32_t n, bool plane
       d.child[k] = m == 0x01u ? s.child[k] * 80 : s.child[k];  // < 2^31 (rt_scene_create)
     }
     for (int a = 0; a < 3; ++a) d.origin[a] = s.origin[a];
-    d.exps = (s.exps & 0xffffffu) | valid << 24;
+    d.exps = signed_exps(s.exps) | valid << 24;
     const uint32_t qlo[3] = {s.q_lo_x, s.q_lo_y, s.q_lo_z}, qhi[3] = {s.q_hi_x, s.q_hi_y, s.q_hi_z};
     for (int a = 0; a < 3; ++a) {
       auto pair = [](uint32_t w, int k) { return f16_code((w >> (8 * k)) & 0xffu) | f16_code((w >> (8 * k + 8)) & 0xffu) << 16; };
