@@ -2046,7 +2046,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(LogicArgs a) {
 // is the unit's hit record (loaded by the caller; unused for a miss).
 template <bool kTex>
 __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit, int res, const HitRec& hr,
-                                              unsigned occl_bits) {
+                                              unsigned occl_bits, const V3* ray_origin = nullptr) {
   if (res < 0) return V3{0.1f, 0.1f, 0.1f};
   const V3 hp = hr.p, hn = hr.n;
   const rt_material& m = a.mats[hr.mat];
@@ -2061,7 +2061,9 @@ __device__ __forceinline__ V3 one_pass_sample(const LogicArgs& a, size_t unit, i
   if (a.n_fuse > 0) {
     const size_t N = (size_t)(unsigned)a.n_slots;
     V3 ro{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
-    if (a.op_fo >= 0) {
+    if (ray_origin) {  // flat_render_kernel: the camera ray it traced itself
+      ro = *ray_origin;
+    } else if (a.op_fo >= 0) {
       const float* Qo = a.query + (size_t)a.op_fo * N + unit;
       ro = V3{Qo[0], Qo[N], Qo[2 * N]};
     }
@@ -2202,6 +2204,117 @@ __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(Logic
     }
     __syncthreads();
   }
+  const int p = p0 + (int)threadIdx.x;
+  if ((int)threadIdx.x >= np) return;
+  int x, y;
+  size_t off;
+  if (!pixel_coords(a, p, x, y, off)) return;
+  V3 c = acc;
+  if (a.spp_sqrt > 1) {  // compute_pixel_color: sum / (float)(s*s) (raytracer.cpp:46-69)
+    const float tot = (float)a.n_samples;
+    c = V3{acc.x / tot, acc.y / tot, acc.z / tot};
+  }
+  a.out[off] = c.x;
+  a.out[off + 1] = c.y;
+  a.out[off + 2] = c.z;
+}
+
+// Few-primitive one-pass calls (r06): the whole sample in one thread -- the camera ray
+// (camera_kernel's ops), its closest hit and its point-light shadow rays against the scene's
+// primitives, and the shading -- with shade_reduce_kernel's per-pixel sums.  A scene of at most
+// RT_FLAT_PRIMS bounded primitives gives every traversal one leaf item of all of them (the trace
+// kernel's root_item), so the traversal kernel's queue, stacks and refill only move a handful of
+// primitive tests around, and camera rays, results and hit records make three HBM round trips
+// per sample.  Here each query runs test_prims over the same leaf item (the exact reference-leaf
+// filter, closest hit by (t, reference index): no order dependence) and over the unbounded
+// primitives (complete_query), the hit record is the fused settle's (finish_query / prim_hit)
+// and the shadow rays are fused_shadow's: the same functions on the same operands, so the
+// same bits.  Rays are counted as the trace kernel counts them (camera + shadow rays).
+template <bool kPlanesOnly>
+__global__ __launch_bounds__(kBlock) void flat_render_kernel(LogicArgs a, TraceArgs t) {
+  __shared__ float stage[kSrPixels * kSrStride];
+  const int p0 = blockIdx.x * kSrPixels;
+  const int np = min(kSrPixels, a.n_pixels - p0);
+  const int ns = a.n_samples;
+  const int nb = t.root_item < 0 && t.root_item != kNoItem ? (int)((uint32_t)t.root_item & 0x7fu) : 0;
+  unsigned int nrays = 0, nprim = 0;
+  auto flat_query = [&](const Query& q, HitState& h) {  // the leaf item of all bounded primitives, then the rest
+    if (nb > 0) test_prims<false, kPlanesOnly>(t, 0, nb, q.r, q.any, q.tmax, q.par, true, h, nprim);
+    complete_query<false, kPlanesOnly>(t, 0, q, h, nprim);
+  };
+  V3 acc{0.0f, 0.0f, 0.0f};
+  for (int s0 = 0; s0 < ns; s0 += kSrChunk) {
+    const int cn = min(kSrChunk, ns - s0), total = np * cn;
+    for (int m = 0; m < kSrUnits; ++m) {
+      const int i = (int)threadIdx.x + m * kBlock;
+      if (i >= total) continue;
+      const int j = cn == kSrChunk ? i / kSrChunk : i / cn, k = i - j * cn;
+      const size_t u = (size_t)(p0 + j) * (size_t)ns + (size_t)(s0 + k);
+      int px, py, sample;
+      uint64_t key;
+      int res = -1;
+      unsigned ob = 0;
+      HitRec hr{};
+      V3 ro{0.0f, 0.0f, 0.0f};
+      if (unit_coords(a, (long long)u, px, py, sample, key)) {
+        Rng rng;
+        const Ray cam = sample_ray(a, px, py, sample, key, rng);
+        const float time = a.op_ft >= 0 ? (float)rng.next() : 0.0f;  // camera_kernel's ray-time draw
+        ro = cam.o;
+        Query q;
+        setup_query(q, cam.o, cam.d, time, false);
+        ++nrays;
+        HitState h{__builtin_inff(), 0x7fffffff, -1, false};
+        flat_query(q, h);
+        res = h.best_idx;
+        if (res >= 0) {
+          const float4* rec = t.c.prims + (size_t)res * t.c.prim_stride4;
+          if constexpr (kPlanesOnly) {  // finish_query's record: o + t d, the plane's normal and tag
+            const float* w = reinterpret_cast<const float*>(rec);
+            hr.p = V3{q.r.o.x + h.best_t * q.r.d.x, q.r.o.y + h.best_t * q.r.d.y, q.r.o.z + h.best_t * q.r.d.z};
+            hr.n = V3{w[3], w[7], w[11]};
+            hr.mat = RT_TAG_MATERIAL(__float_as_uint(w[15]));
+          } else {  // the fused settle's record
+            PrimA P;
+            load_prim_a(rec, P);
+            HitAttr at;
+            float th;
+            prim_hit<true, false, false>(P, rec, q.r, th, &at);
+            hr.p = at.p;
+            hr.n = at.n;
+            hr.mat = RT_TAG_MATERIAL(prim_tag(P));
+          }
+          for (int l = 0; l < t.n_fuse; ++l) {  // fused_shadow
+            const rt_light& L = t.lights[l];
+            const V3 lv = sub(V3{L.location[0], L.location[1], L.location[2]}, hr.p);
+            const float tmax = sqrtf(dot(lv, lv));
+            Query sq;
+            setup_query(sq, add(hr.p, mul(hr.n, 1e-4f)), normalize(lv), tmax, true);
+            ++nrays;
+            HitState sh{__builtin_inff(), 0x7fffffff, -1, false};
+            flat_query(sq, sh);
+            if (sh.done) ob |= 1u << l;
+          }
+        }
+      }
+      const V3 c = one_pass_sample<false>(a, u, res, hr, ob, &ro);
+      float* d = stage + j * kSrStride + k * 3;
+      d[0] = c.x;
+      d[1] = c.y;
+      d[2] = c.z;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      const float* q = stage + threadIdx.x * kSrStride;
+      if (a.spp_sqrt <= 1) acc = V3{q[0], q[1], q[2]};
+      else
+        for (int k = 0; k < cn * 3; k += 3) acc = V3{acc.x + q[k], acc.y + q[k + 1], acc.z + q[k + 2]};
+    }
+    __syncthreads();
+  }
+  unsigned long long nr = nrays;
+  for (int off = 32; off > 0; off >>= 1) nr += __shfl_xor(nr, off);
+  if ((threadIdx.x & 63) == 0 && nr) atomicAdd(t.rays, nr);
   const int p = p0 + (int)threadIdx.x;
   if ((int)threadIdx.x >= np) return;
   int x, y;
@@ -3504,20 +3617,33 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     P.ta.any_query = aq;
     P.ta.host_flag = s->h_flag;
     P.ta.n_work = (int)n_units;
-    hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
-    HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
-    launch_trace(P.ta, p->count_work != 0, planes_only, false, seven, fixed, P.trace_blocks, lds, stream);
-    HIP_TRY(hipGetLastError(), RT_EDEVICE);
-    HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
     const unsigned rblocks = (unsigned)((n_pixels + kSrPixels - 1) / kSrPixels);
-    if (tex) hipLaunchKernelGGL((shade_reduce_kernel<true, kHitRecord>), dim3(rblocks), dim3(kBlock), 0, stream, la);
-    else if (ta.has_tex == kHitCompact)
-      hipLaunchKernelGGL((shade_reduce_kernel<false, kHitCompact>), dim3(rblocks), dim3(kBlock), 0, stream, la);
-    else if (ta.has_tex == kHitRecompute)
-      hipLaunchKernelGGL((shade_reduce_kernel<false, kHitRecompute>), dim3(rblocks), dim3(kBlock), 0, stream, la);
-    else hipLaunchKernelGGL((shade_reduce_kernel<false, kHitRecord>), dim3(rblocks), dim3(kBlock), 0, stream, la);
-    HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    // scenes whose every traversal is one leaf item of all their bounded primitives (root_item,
+    // RT_FLAT_PRIMS) and no textures: the whole sample in one kernel (flat_render_kernel; its
+    // time is the call's trace time); the instrumented and tile-measuring calls keep the launches
+    const bool flat_render = !tex && !p->count_work && !measure_tiles && ta.c.use_bvh && ta.root_item < 0 &&
+                             ta.root_item != kNoItem && knob(K_FLAT_RENDER, 1) != 0;
+    if (flat_render) {
+      HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
+      if (planes_only) hipLaunchKernelGGL((flat_render_kernel<true>), dim3(rblocks), dim3(kBlock), 0, stream, la, P.ta);
+      else hipLaunchKernelGGL((flat_render_kernel<false>), dim3(rblocks), dim3(kBlock), 0, stream, la, P.ta);
+      HIP_TRY(hipGetLastError(), RT_EDEVICE);
+      HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
+    } else {
+      hipLaunchKernelGGL(camera_kernel, dim3((unsigned)((n_units + kBlock - 1) / kBlock)), dim3(kBlock), 0, stream, P.la);
+      HIP_TRY(hipGetLastError(), RT_EDEVICE);
+      HIP_TRY(hipEventRecord(s->ev_a[0][0], stream), RT_EDEVICE);
+      launch_trace(P.ta, p->count_work != 0, planes_only, false, seven, fixed, P.trace_blocks, lds, stream);
+      HIP_TRY(hipGetLastError(), RT_EDEVICE);
+      HIP_TRY(hipEventRecord(s->ev_b[0][0], stream), RT_EDEVICE);
+      if (tex) hipLaunchKernelGGL((shade_reduce_kernel<true, kHitRecord>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+      else if (ta.has_tex == kHitCompact)
+        hipLaunchKernelGGL((shade_reduce_kernel<false, kHitCompact>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+      else if (ta.has_tex == kHitRecompute)
+        hipLaunchKernelGGL((shade_reduce_kernel<false, kHitRecompute>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+      else hipLaunchKernelGGL((shade_reduce_kernel<false, kHitRecord>), dim3(rblocks), dim3(kBlock), 0, stream, la);
+      HIP_TRY(hipGetLastError(), RT_EDEVICE);
+    }
     HIP_TRY(hipMemcpyAsync(h_stats, ctl, kStatsBytes, hipMemcpyDeviceToHost, stream), RT_EDEVICE);
     if (measure_tiles)
       HIP_TRY(hipMemcpyAsync(s->h_tile_cost, s->d_tile_cost, (size_t)n_tiles * 8, hipMemcpyDeviceToHost, stream),

@@ -26,6 +26,7 @@ enum Knob : int {
   K_SHADOW_STEP,    // 0 (with RT_SOFT_FUSE=0): soft samples advanced by the logic kernel itself
   K_COMPACT_HIT,    // 0: one-pass planes calls store the 32-B hit record instead of the hit's t
   K_FLAT_PRIMS,     // scenes of at most this many bounded primitives test them all, no traversal (default 8)
+  K_FLAT_RENDER,    // 0: one-pass calls of such scenes keep camera / traversal / shading launches (default 1: one kernel)
   // traversal scheduling
   K_FETCH_SHARDS,   // trace work counters (default 32)
   K_BATCH_SHARDS,   // step pipeline: batch-claim counters (default 128)
@@ -55,7 +56,7 @@ static constexpr KnobDef kKnobDefs[K_COUNT] = {
     {"RT_ONE_PASS", 0, 1},        {"RT_ONE_PASS_MAX", 1, 1LL << 30}, {"RT_MAX_UNITS", 1, 1LL << 30},
     {"RT_SLOTS", 1LL << 12, 1LL << 31}, {"RT_PIPES", 1, 4},          {"RT_FUSE", 0, 1},
     {"RT_SOFT_FUSE", 0, 1},       {"RT_SOFT_START", 0, 1},           {"RT_SHADOW_STEP", 0, 1},
-    {"RT_COMPACT_HIT", 0, 1},     {"RT_FLAT_PRIMS", 0, 1 << 20},
+    {"RT_COMPACT_HIT", 0, 1},     {"RT_FLAT_PRIMS", 0, 1 << 20},     {"RT_FLAT_RENDER", 0, 1},
     {"RT_FETCH_SHARDS", 1, 256},  {"RT_BATCH_SHARDS", 1, 1024},      {"RT_LEAF_MIN", 1, 64},
     {"RT_REFILL", 1, 64},         {"RT_LDS_STACK", 1, 64},           {"RT_TRACE_SEVEN", 0, 1},
     {"RT_DRAIN_HELP", 0, 1},      {"RT_XCD_CHUNK", 0, 1LL << 20},    {"RT_TILE_ORDER", 0, 1},

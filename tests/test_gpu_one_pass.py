@@ -14,7 +14,10 @@ instance computing the hit record alone), a moving sphere (the ray time), a thin
 camera (stored origins), tiles reaching past the image (the kind word), several lights.
 Every case also renders with RT_COMPACT_HIT=0: the trace kernel stores the 32-B hit record
 instead of the hit's t (planes) or nothing (transformed shapes: shade_reduce_kernel recomputes
-the hit, r06), and both must give the oracle's bits.
+the hit, r06), and both must give the oracle's bits; and with RT_FLAT_RENDER=0: scenes of at
+most 8 bounded primitives (the shapes and antialiasing cases) render by default in one kernel
+per call (flat_render_kernel: camera ray, queries and shading per thread, r06), with the knob
+through the camera / traversal / shading launches.
 Reference: Code/raytracer.cpp:18-70 (compute_pixel_color), :180-274 (shade), :280-351 (Trace).
 """
 import copy
@@ -117,7 +120,8 @@ def test_one_pass_matches_oracle(name, tmp_path, gpu):
     chunk = str(64 * 64 * spp_sqrt * spp_sqrt)
     for env, path_kind in (({}, rt.PATH_ONE_PASS), ({"RT_ONE_PASS": "0"}, rt.PATH_STEPS),
                            ({"RT_ONE_PASS_MAX": chunk}, rt.PATH_ONE_PASS),
-                           ({"RT_COMPACT_HIT": "0"}, rt.PATH_ONE_PASS)):
+                           ({"RT_COMPACT_HIT": "0"}, rt.PATH_ONE_PASS),
+                           ({"RT_FLAT_RENDER": "0"}, rt.PATH_ONE_PASS)):
         img, st = _render(path, spp_sqrt, env)
         assert st.path == path_kind, (name, env, st.path)
         bad = int((img.view(np.uint32) != ref.view(np.uint32)).sum())
