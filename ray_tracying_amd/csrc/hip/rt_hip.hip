@@ -271,6 +271,14 @@ struct LogicArgs {
   // the direction in fields 0..2, then (-1: absent) the origin (thin lens), the ray time
   // (transformed shapes: moving spheres) and a kind word (some tile reaches past the image)
   int op_fo, op_ft, op_fk;
+  // step-pipeline calls of few-primitive scenes (kInline logic instances, r06): the logic step
+  // answers the queries it emits itself -- one leaf item of the flat_n bounded primitives and the
+  // unbounded ones, as the trace kernel's flat root item does -- and counts them in *rays
+  const int2* prim_refs;
+  const float4* ref_boxes;
+  int n_unbounded;
+  int flat_n;
+  unsigned long long* rays;
 };
 
 #ifndef RT_XCD_CHUNK_DEFAULT
@@ -1464,8 +1472,19 @@ __device__ __forceinline__ V3 diffuse_color(const LogicArgs& a, const rt_materia
 #endif
 // kRefr: the scene has refraction (pending refraction rays in the frames); the reflection-only
 // instance of the frames variant drops that code and fits 4 waves/SIMD (121 VGPRs, 161 with it)
-template <bool kFrames, bool kRefr, bool kTex, bool kPlanes>
-__global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
+// kInline: a few-primitive scene (at most RT_FLAT_PRIMS bounded primitives: every traversal is
+// one leaf item of all of them) -- the step answers every query it emits itself, against that
+// leaf item and the unbounded primitives with the trace kernel's functions (test_prims,
+// complete_query, the hit record of finish_query / the ST_CLOSEST entry below), and goes on
+// with the sample: a slot's sample runs to its end in one step, and the traversal launches only
+// answer the camera queries start_kernel emits (and the soft-light chains they start).  The
+// answers are the trace kernel's (same functions, same operands), the shadow rays the unfused
+// ones (RT_FUSE=0 / RT_SOFT_FUSE=0 order of draws: the knob tests pin them equal), so the same bits.
+#ifndef RT_LOGIC_WAVES_I
+#define RT_LOGIC_WAVES_I 5
+#endif
+template <bool kFrames, bool kRefr, bool kTex, bool kPlanes, bool kInline = false>
+__global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : kInline ? RT_LOGIC_WAVES_I : RT_LOGIC_WAVES) void logic_kernel(LogicArgs a) {
   const int slot = a.slot_base + (int)(blockIdx.x * kBlock + threadIdx.x);
   // a wave whose slots all retired has nothing left in this frame (one scalar load)
   if (a.wave_done[__builtin_amdgcn_readfirstlane(slot >> 6)] != 0u) return;
@@ -1475,6 +1494,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
   const unsigned claimed = __hip_atomic_load(a.batch_ctr + shard * kCtrStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool no_batch = ((long long)claimed * a.batch_shards + shard) * 64 >= a.n_units;
   bool want = false;
+  unsigned int n_inline = 0;  // kInline: queries answered by this step
   if (slot < a.slot_end) {
     const int N = a.n_slots;
     uint32_t* S = a.state;
@@ -1575,7 +1595,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
           ray.o = cam_o;
         }
       }
-      const int res = st0 >= ST_CLOSEST ? res_ld : -1;
+      int res = st0 >= ST_CLOSEST ? res_ld : -1;
       // later steps of a sample continue its RNG stream from the stored key and counter
       Rng rng;
       rng.key = 0;
@@ -1586,12 +1606,13 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
       }
       bool idle = st0 < 0;  // idle (batch done, pixel outside the image): start_kernel's work
       // a closest hit whose point-light shadow rays the trace kernel traced along (kFuse)
-      const bool fused = a.n_fuse > 0 && st0 == ST_CLOSEST && res >= 0;
+      bool fused = a.n_fuse > 0 && st0 == ST_CLOSEST && res >= 0;
       const unsigned occl_bits = fused ? a.occl[slot] : 0u;
       V3 qo{0, 0, 0}, qd{0, 0, 0};
       float qtmax = 0.0f;
       int qkind = 0;
 
+      for (;;) {
       while (!want && !idle) {
         V3 ret{0, 0, 0};
         bool returning = false;
@@ -1798,6 +1819,50 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
           }
         }
       }
+      if (!kInline || !want) break;
+      if constexpr (kInline) {  // answer the query just emitted and go on with the sample
+        TraceArgs tv{};  // what test_prims / complete_query read
+        tv.c = a.c;
+        tv.prim_refs = a.prim_refs;
+        tv.ref_boxes = a.ref_boxes;
+        tv.n_unbounded = a.n_unbounded;
+        Query q;
+        setup_query(q, qo, qd, qtmax, qkind == 1);
+        ++n_inline;
+        HitState h{__builtin_inff(), 0x7fffffff, -1, false};
+        unsigned int np = 0;
+        if (a.flat_n > 0) test_prims<false, kPlanes>(tv, 0, a.flat_n, q.r, q.any, q.tmax, q.par, true, h, np);
+        complete_query<false, kPlanes>(tv, slot, q, h, np);
+        want = false;
+        if (qkind == 1) {  // shadow: occluded (st is ST_SHADOW)
+          res = h.done ? 1 : 0;
+        } else {  // closest (st is ST_CLOSEST): the hit record the entry above would read
+          res = h.best_idx;
+          fused = false;  // its shadow rays are this step's own queries
+          ray = q.r;      // closest queries carry the ray time in qtmax (0 for secondary rays)
+          if (res >= 0) {
+            const float4* rec = a.c.prims + (size_t)res * a.c.prim_stride4;
+            if constexpr (kPlanes && !kTex) {  // finish_query: o + t d, the plane's normal and tag
+              const float* w = reinterpret_cast<const float*>(rec);
+              hp = V3{q.r.o.x + h.best_t * q.r.d.x, q.r.o.y + h.best_t * q.r.d.y, q.r.o.z + h.best_t * q.r.d.z};
+              hn = V3{w[3], w[7], w[11]};
+              mat_id = (int)RT_TAG_MATERIAL(__float_as_uint(w[15]));
+            } else {  // prim_hit with attributes (finish_query's textured planes, the entry's shapes)
+              PrimA P;
+              load_prim_a(rec, P);
+              HitAttr at;
+              float th;
+              prim_hit<true, kPlanes, kTex>(P, rec, q.r, th, &at);
+              hp = at.p;
+              hn = at.n;
+              hu = at.u;
+              hv = at.v;
+              mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
+            }
+          }
+        }
+      }
+      }
       const bool wave_wants_here = __ballot(want) != 0ull;  // lanes outside this block want nothing
       if (fast || st0 < 0) {
         // advanced by shadow_step_kernel / idle since an earlier step: nothing changes
@@ -1839,6 +1904,11 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : RT_LOGIC_WAVES) 
     } else {
       a.wave_done[wave] = no_batch ? 1u : kWaveIdle;
     }
+  }
+  if constexpr (kInline) {  // the queries answered here, counted as the trace kernel counts its own
+    unsigned long long nr = n_inline;
+    for (int off = 32; off > 0; off >>= 1) nr += __shfl_xor(nr, off);
+    if ((threadIdx.x & 63) == 0 && nr) atomicAdd(a.rays, nr);
   }
 }
 
@@ -2368,9 +2438,15 @@ __global__ __launch_bounds__(kBlock) void init_kernel(InitArgs a) {
 }
 
 template <bool F, bool R, bool T>
-void launch_logic2(const LogicArgs& la, bool planes, unsigned blocks, hipStream_t st) {
-  if (planes) hipLaunchKernelGGL((logic_kernel<F, R, T, true>), dim3(blocks), dim3(kBlock), 0, st, la);
-  else hipLaunchKernelGGL((logic_kernel<F, R, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
+void launch_logic2(const LogicArgs& la, bool planes, bool inl, unsigned blocks, hipStream_t st) {
+  if (inl && !T) {  // few-primitive scenes without textures: queries answered in the step
+    if (planes) hipLaunchKernelGGL((logic_kernel<F, R, T, true, !T>), dim3(blocks), dim3(kBlock), 0, st, la);
+    else hipLaunchKernelGGL((logic_kernel<F, R, T, false, !T>), dim3(blocks), dim3(kBlock), 0, st, la);
+  } else if (planes) {
+    hipLaunchKernelGGL((logic_kernel<F, R, T, true>), dim3(blocks), dim3(kBlock), 0, st, la);
+  } else {
+    hipLaunchKernelGGL((logic_kernel<F, R, T, false>), dim3(blocks), dim3(kBlock), 0, st, la);
+  }
 }
 // trace launch (the refill kernel; count: the instrumented variant)
 template <bool kCount, bool kFixed>
@@ -2413,16 +2489,17 @@ static int batch_shards_env() { return (int)knob(K_BATCH_SHARDS, 128); }
 static int leaf_min_env() { return (int)knob(K_LEAF_MIN, kLeafDefault); }
 static int refill_min_env() { return (int)knob(K_REFILL, kRefillDefault); }
 
-void launch_logic(const LogicArgs& la, bool frames, bool refr, bool tex, bool planes, unsigned blocks, hipStream_t st) {
+void launch_logic(const LogicArgs& la, bool frames, bool refr, bool tex, bool planes, bool inl, unsigned blocks,
+                  hipStream_t st) {
   if (frames && refr) {
-    if (tex) launch_logic2<true, true, true>(la, planes, blocks, st);
-    else launch_logic2<true, true, false>(la, planes, blocks, st);
+    if (tex) launch_logic2<true, true, true>(la, planes, inl, blocks, st);
+    else launch_logic2<true, true, false>(la, planes, inl, blocks, st);
   } else if (frames) {
-    if (tex) launch_logic2<true, false, true>(la, planes, blocks, st);
-    else launch_logic2<true, false, false>(la, planes, blocks, st);
+    if (tex) launch_logic2<true, false, true>(la, planes, inl, blocks, st);
+    else launch_logic2<true, false, false>(la, planes, inl, blocks, st);
   } else {
-    if (tex) launch_logic2<false, false, true>(la, planes, blocks, st);
-    else launch_logic2<false, false, false>(la, planes, blocks, st);
+    if (tex) launch_logic2<false, false, true>(la, planes, inl, blocks, st);
+    else launch_logic2<false, false, false>(la, planes, inl, blocks, st);
   }
 }
 
@@ -3395,6 +3472,16 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
     ta.root_item = flat ? (int)(0x80000000u | (uint32_t)n_bounded)  // a leaf item: kLeafBit | first 0 << 7 | count
                    : (s->desc.n_prims > 0 && p->use_bvh && s->desc.n_nodes > 0) ? 0 : -1;
   }
+  // ... and on the step pipeline (no textures) the logic step answers the queries it emits itself
+  // (kInline logic instances, r06; RT_FLAT_RENDER=0: every query through the traversal launches;
+  // the instrumented frame keeps them for its counts)
+  const bool flat_item = ta.root_item < 0 && ta.root_item != kNoItem;
+  la.prim_refs = ta.prim_refs;
+  la.ref_boxes = ta.ref_boxes;
+  la.n_unbounded = ta.n_unbounded;
+  la.rays = ta.rays;
+  la.flat_n = flat_item ? (int)((uint32_t)ta.root_item & 0x7fu) : 0;
+  const bool inline_queries = !one_pass && flat_item && !p->count_work && knob(K_FLAT_RENDER, 1) != 0;
   for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
   ta.light_samples = p->light_samples;
   // the closest hit starts its shade loop in the tracing lane too: planes, or untextured
@@ -3687,7 +3774,7 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
             hipLaunchKernelGGL(shadow_step_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
             HIP_TRY(hipGetLastError(), RT_EDEVICE);
           }
-          launch_logic(P.la, need_frames, need_refr, tex, planes_only, P.logic_blocks, P.st);
+          launch_logic(P.la, need_frames, need_refr, tex, planes_only, inline_queries, P.logic_blocks, P.st);
           HIP_TRY(hipGetLastError(), RT_EDEVICE);
         }
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);

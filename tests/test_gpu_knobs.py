@@ -70,7 +70,9 @@ KNOBS = [
     {"RT_XCD_CHUNK": "1048576"},  # the clamp bound (2^20 groups per chunk)
     {"RT_COMPACT_HIT": "0"},  # one-pass planes calls store the 32-B hit record instead of the hit's t
     {"RT_FLAT_PRIMS": "127"},  # scenes of <= 127 primitives (features) test them all from one leaf item
-    {"RT_FLAT_PRIMS": "127", **STEPS},  # ... through the step pipeline
+    {"RT_FLAT_PRIMS": "127", **STEPS},  # ... through the step pipeline (the logic step answers its own queries)
+    {"RT_FLAT_PRIMS": "127", "RT_FLAT_RENDER": "0"},  # ... every query through the traversal launches
+    {"RT_FLAT_PRIMS": "127", "RT_FLAT_RENDER": "0", **STEPS},
     # step-pipeline knobs on a one-pass scene: ignored (one message each), still one-pass
     {"RT_FUSE": "1"},
     {"RT_FUSE": "0", "RT_SLOTS": "4096", "RT_PIPES": "2", "RT_DIAG": "1"},
