@@ -1473,13 +1473,13 @@ __device__ __forceinline__ V3 diffuse_color(const LogicArgs& a, const rt_materia
 // kRefr: the scene has refraction (pending refraction rays in the frames); the reflection-only
 // instance of the frames variant drops that code and fits 4 waves/SIMD (121 VGPRs, 161 with it)
 // kInline: a few-primitive scene (at most RT_FLAT_PRIMS bounded primitives: every traversal is
-// one leaf item of all of them) -- the step answers every query it emits itself, against that
-// leaf item and the unbounded primitives with the trace kernel's functions (test_prims,
-// complete_query, the hit record of finish_query / the ST_CLOSEST entry below), and goes on
-// with the sample: a slot's sample runs to its end in one step, and the traversal launches only
-// answer the camera queries start_kernel emits (and the soft-light chains they start).  The
-// answers are the trace kernel's (same functions, same operands), the shadow rays the unfused
-// ones (RT_FUSE=0 / RT_SOFT_FUSE=0 order of draws: the knob tests pin them equal), so the same bits.
+// one leaf item of all of them) -- the step answers every query itself, the camera query
+// start_kernel emitted and every one it emits, against that leaf item and the unbounded
+// primitives with the trace kernel's functions (test_prims, complete_query, the hit record of
+// finish_query / the ST_CLOSEST entry below), and goes on with the sample: a slot's sample runs
+// to its end in one step and the call launches no traversal at all.  The answers are the trace
+// kernel's (same functions, same operands), the shadow rays the unfused ones (the RT_FUSE=0 /
+// RT_SOFT_FUSE=0 / RT_SOFT_START=0 order of draws: the knob tests pin them equal), so the same bits.
 #ifndef RT_LOGIC_WAVES_I
 #define RT_LOGIC_WAVES_I 5
 #endif
@@ -1508,7 +1508,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : kInline ? RT_LOG
     // discards them), so no load waits on another's value before the state-specific round.
     long long unit = (long long)(int)ld(F_UNIT);  // >= 0 active, -2 idle (batch done), -1 retired
     const uint32_t ctrl0 = ld(F_CTRL);
-    const int res_ld = a.result[slot];
+    const int res_ld = kInline ? -1 : a.result[slot];  // kInline: no traversal launch answered anything
     uint32_t key_lo = 0, key_hi = 0, rng_ctr = 0;
     if (a.late_draws) {
       key_lo = ld(F_KEY);
@@ -1538,7 +1538,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : kInline ? RT_LOG
       const V3 cam_o{a.cam.location[0], a.cam.location[1], a.cam.location[2]};
       if (fast) {
         want = true;
-      } else if (!kPlanes && st0 == ST_CLOSEST && res_ld >= 0 && a.n_fuse == 0) {
+      } else if (!kInline && !kPlanes && st0 == ST_CLOSEST && res_ld >= 0 && a.n_fuse == 0) {
         // the hit being shaded (raytracer.cpp:293-303): the hit primitive's test with
         // attributes on the ray just traced (the query record), kept in the slot's hit record
         // for the shadow steps that follow
@@ -1557,7 +1557,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : kInline ? RT_LOG
         mat_id = (int)RT_TAG_MATERIAL(prim_tag(P));
         store_hit_pnm(hit_rec(a.hit, slot), hp, hn, (uint32_t)mat_id);
         if (kTex) a.hit_uv[slot] = make_float2(hu, hv);
-      } else if (st0 == ST_SHADOW || (st0 == ST_CLOSEST && res_ld >= 0)) {
+      } else if (!kInline && (st0 == ST_SHADOW || (st0 == ST_CLOSEST && res_ld >= 0))) {
         // the hit being shaded: its record (written by the trace kernel for planes-only scenes,
         // by the ST_CLOSEST step above otherwise); a closest miss does not read it
         const HitRec hr = load_hit(hit_rec(a.hit, slot));
@@ -1583,7 +1583,7 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : kInline ? RT_LOG
         }
         if (ls > 0) vis = ldf(F_VIS);
         if (light > 0) fin = V3{ldf(F_FIN), ldf(F_FIN + 1), ldf(F_FIN + 2)};
-      } else if (st0 == ST_CLOSEST) {
+      } else if (!kInline && st0 == ST_CLOSEST) {
         if (kFrames) {
           const QueryRec qr = load_query(a.query, N, slot, a.cam.location);
           ray.o = qr.o;
@@ -1606,11 +1606,18 @@ __global__ __launch_bounds__(kBlock, kRefr ? RT_LOGIC_WAVES_F : kInline ? RT_LOG
       }
       bool idle = st0 < 0;  // idle (batch done, pixel outside the image): start_kernel's work
       // a closest hit whose point-light shadow rays the trace kernel traced along (kFuse)
-      bool fused = a.n_fuse > 0 && st0 == ST_CLOSEST && res >= 0;
+      bool fused = !kInline && a.n_fuse > 0 && st0 == ST_CLOSEST && res >= 0;
       const unsigned occl_bits = fused ? a.occl[slot] : 0u;
       V3 qo{0, 0, 0}, qd{0, 0, 0};
       float qtmax = 0.0f;
       int qkind = 0;
+      if (kInline && st0 == ST_CLOSEST) {  // the camera query start_kernel emitted: answered below
+        const QueryRec qr = load_query(a.query, N, slot, a.cam.location);
+        qo = qr.o;
+        qd = qr.d;
+        qtmax = qr.tq;
+        want = true;
+      }
 
       for (;;) {
       while (!want && !idle) {
@@ -2399,6 +2406,10 @@ __global__ __launch_bounds__(kBlock) void flat_render_kernel(LogicArgs a, TraceA
   a.out[off + 1] = c.y;
   a.out[off + 2] = c.z;
 }
+
+// kInline calls launch no traversal: the host's per-step flag (the trace kernel's first store
+// otherwise) -- start_kernel emitted camera queries, so the next step has samples to run
+__global__ void step_flag_kernel(const unsigned int* any_query, unsigned int* host_flag) { *host_flag = *any_query; }
 
 // pixel finalisation (raytracer.cpp:446-457, image.cpp:28-37), the same ops as rth_quantise
 __global__ __launch_bounds__(kBlock) void quantise_kernel(const float* rgb, long long n, uint8_t* out) {
@@ -3481,7 +3492,8 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
   la.n_unbounded = ta.n_unbounded;
   la.rays = ta.rays;
   la.flat_n = flat_item ? (int)((uint32_t)ta.root_item & 0x7fu) : 0;
-  const bool inline_queries = !one_pass && flat_item && !p->count_work && knob(K_FLAT_RENDER, 1) != 0;
+  const bool inline_queries = !one_pass && flat_item && !p->count_work && knob(K_FLAT_RENDER, 1) != 0 &&
+                              (s->desc.flags & RT_SCENE_HAS_TEXTURE) == 0;  // (launch_logic2: untextured instances)
   for (int k = 0; k < 3; ++k) ta.cam_loc[k] = cam->location[k];
   ta.light_samples = p->light_samples;
   // the closest hit starts its shade loop in the tracing lane too: planes, or untextured
@@ -3774,15 +3786,26 @@ static int render_tiles(rt_scene_t s, const rt_camera_desc* cam, const rt_render
             hipLaunchKernelGGL(shadow_step_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
             HIP_TRY(hipGetLastError(), RT_EDEVICE);
           }
+          // (kInline: the logic step does the traversal work -- the step's logic, start and flag
+          // launches are its trace time, and the host's wait on ev_b covers the flag's store)
+          if (inline_queries) HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
           launch_logic(P.la, need_frames, need_refr, tex, planes_only, inline_queries, P.logic_blocks, P.st);
           HIP_TRY(hipGetLastError(), RT_EDEVICE);
+        } else if (inline_queries) {
+          HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
         }
         hipLaunchKernelGGL(start_kernel, dim3(P.logic_blocks), dim3(kBlock), 0, P.st, P.la);
         HIP_TRY(hipGetLastError(), RT_EDEVICE);
-        HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
-        launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, seven, fixed, P.trace_blocks, lds, P.st);
-        HIP_TRY(hipGetLastError(), RT_EDEVICE);
-        HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
+        if (inline_queries) {
+          hipLaunchKernelGGL(step_flag_kernel, dim3(1), dim3(1), 0, P.st, (const unsigned int*)aq, P.ta.host_flag);
+          HIP_TRY(hipGetLastError(), RT_EDEVICE);
+          HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
+        } else {
+          HIP_TRY(hipEventRecord(s->ev_a[h][k], P.st), RT_EDEVICE);
+          launch_trace(P.ta, p->count_work != 0, planes_only, soft_trace, seven, fixed, P.trace_blocks, lds, P.st);
+          HIP_TRY(hipGetLastError(), RT_EDEVICE);
+          HIP_TRY(hipEventRecord(s->ev_b[h][k], P.st), RT_EDEVICE);
+        }
       }
     }
     int enq = 0;

@@ -79,12 +79,24 @@ KNOBS = [
 ]
 
 
-@pytest.mark.parametrize("scene", ["soup", "features"])
+def _untextured(sc):
+    """features() without its textures: the step pipeline's untextured logic instances, whose
+    few-primitive form (RT_FLAT_PRIMS=127 here) answers its own queries (kInline, r06)."""
+    for kind in ("spheres", "cubes", "rectangles", "planes"):
+        for o in sc.get(kind, []):
+            if o.get("material"):
+                o["material"].pop("texture_file", None)
+    return sc
+
+
+@pytest.mark.parametrize("scene", ["soup", "features", "features_untextured"])
 def test_knobs_do_not_change_results(scene, tmp_path, gpu):
     if scene == "soup":
         p = scenes.write(scenes.soup(3000, seed=11, res=(48, 48)), str(tmp_path / "s.json"))
-    else:  # reflection, refraction, soft shadows, textures, every primitive kind
+    elif scene == "features":  # reflection, refraction, soft shadows, textures, every primitive kind
         p = scenes.write(scenes.features(res=(40, 32)), str(tmp_path / "f.json"))
+    else:
+        p = scenes.write(_untextured(scenes.features(res=(40, 32))), str(tmp_path / "fu.json"))
     ref, _, ost = ob.render(p, rng=ob.RNG_COUNTER, seed=5, spp_sqrt=2, light_samples=2, use_bvh=True,
                             texture_root=scenes.TEXTURES)
     for i, env in enumerate(KNOBS):
