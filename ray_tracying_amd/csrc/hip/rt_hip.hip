@@ -2307,8 +2307,11 @@ __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(Logic
 // primitives (complete_query), the hit record is the fused settle's (finish_query / prim_hit)
 // and the shadow rays are fused_shadow's: the same functions on the same operands, so the
 // same bits.  Rays are counted as the trace kernel counts them (camera + shadow rays).
+#ifndef RT_FLAT_WAVES
+#define RT_FLAT_WAVES 1  // minimum blocks per CU the allocation must allow (1: the compiler's choice)
+#endif
 template <bool kPlanesOnly>
-__global__ __launch_bounds__(kBlock) void flat_render_kernel(LogicArgs a, TraceArgs t) {
+__global__ __launch_bounds__(kBlock, RT_FLAT_WAVES) void flat_render_kernel(LogicArgs a, TraceArgs t) {
   __shared__ float stage[kSrPixels * kSrStride];
   const int p0 = blockIdx.x * kSrPixels;
   const int np = min(kSrPixels, a.n_pixels - p0);
