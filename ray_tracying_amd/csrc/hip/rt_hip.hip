@@ -58,7 +58,13 @@ constexpr int kBlock = 256;
 // render_tiles launches them when a call's values are exactly these (any tree depth: a shallow
 // tree leaves the rows past its depth unused), else the runtime-knob instances (RT_REFILL,
 // RT_LEAF_MIN, RT_LDS_STACK, and the soft-light chains)
-constexpr int kSevenStack = 11, kRefillDefault = 48, kLeafDefault = 24;
+#ifndef RT_REFILL_DEFAULT
+#define RT_REFILL_DEFAULT 48
+#endif
+#ifndef RT_LEAF_DEFAULT
+#define RT_LEAF_DEFAULT 24
+#endif
+constexpr int kSevenStack = 11, kRefillDefault = RT_REFILL_DEFAULT, kLeafDefault = RT_LEAF_DEFAULT;
 constexpr int default_stack(int waves) { return waves >= 7 ? kSevenStack : waves == 6 ? 12 : 16; }
 static int lds_stack_entries(int waves) { return (int)knob(K_LDS_STACK, default_stack(waves)); }
 // LDS stack entries of a launch: the instance's default rows even for a tree shallower than
