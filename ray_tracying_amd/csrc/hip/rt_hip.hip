@@ -78,13 +78,16 @@ static int call_lds_entries(int stack_bound, int waves, bool soft) {
 constexpr int kMaxFetchShards = 256;  // trace work counters (slot slices), one 128-B line each
 constexpr int kFetchStride = 32;      // u32 words between counters
 constexpr int kCtlBytes = 4096;    // control block (cleared by init_kernel)
-constexpr int kStatsBytes = 512;
+constexpr int kStatsBytes = 512;  // its head, copied to the host after each batch: counters at bytes 16..32, 488
 // scenes with fewer primitives spend their frame in the per-step passes over the slots, not in
 // traversal: their shadow rays are fused whatever the call size
 constexpr int kFuseFewPrims = 65536;
 // scenes of at most this many bounded primitives skip the traversal (TraceArgs::root_item;
-// RT_FLAT_PRIMS overrides, 0 = always traverse)
-constexpr int kFlatPrims = 8;   // its head, copied to the host after each batch: counters at bytes 16..32, 488
+// RT_FLAT_PRIMS overrides, 0 = always traverse).  r06 sweep with the one-kernel paths
+// (profiles/r06ao_flat_prims_sweep.txt, exported Blender scenes on the step pipeline):
+// Distributed (10 bounded) 8,608 -> 19,202 Mrays/s flat, Test1 (21) 9,706 -> 8,413 -- 16
+// sits between the two
+constexpr int kFlatPrims = 16;
 // Batch-claim counters of the logic step: one per 128-B line (kCtrStride words apart) --
 // atomics on one line serialise at the memory side, so the shards must not share lines.
 constexpr int kMaxBatchShards = 1024;
