@@ -598,8 +598,11 @@ __device__ __forceinline__ bool unit_coords(const LogicArgs& a, long long unit, 
 // py) -- its RNG stream (keyed by the frame's seed), the stratified jitter in double,
 // Camera::pixelToRay_thin_lens (the lens draws for an aperture > 0).  The ray's time is the
 // caller's next draw.
-__device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, int sample, uint64_t key, Rng& rng) {
-  rng.begin(key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
+// (draws = false: the caller knows the sample draws nothing -- one spp, a pinhole, no ray time
+// -- and the stream's key, two splitmix64 rounds of quarter-rate 64-bit multiplies, is skipped)
+__device__ __forceinline__ Ray sample_ray(const LogicArgs& a, int px, int py, int sample, uint64_t key, Rng& rng,
+                                          bool draws = true) {
+  if (draws) rng.begin(key, (uint64_t)py * (uint64_t)a.cam.res_x + (uint64_t)px, (uint64_t)sample);
   const int s = a.spp_sqrt;
   float fx, fy;
   if (s <= 1) {
@@ -1949,7 +1952,7 @@ __global__ __launch_bounds__(kBlock) void camera_kernel(LogicArgs a) {
     return;
   }
   Rng rng;
-  const Ray ray = sample_ray(a, px, py, sample, key, rng);
+  const Ray ray = sample_ray(a, px, py, sample, key, rng, a.spp_sqrt > 1 || a.cam.aperture > 0.0f || a.op_ft >= 0);
   Q[u] = ray.d.x;
   Q[N + u] = ray.d.y;
   Q[2 * N + u] = ray.d.z;
@@ -2267,7 +2270,10 @@ __global__ __launch_bounds__(kBlock, RT_SR_WAVES) void shade_reduce_kernel(Logic
     HitRec hr[kSrUnits];
 #pragma unroll
     for (int m = 0; m < kSrUnits; ++m) {
-      if constexpr (kHit == kHitCompact) hr[m] = res[m] >= 0 ? compact_hit(a, u[m], res[m]) : HitRec{};
+      if constexpr (kHit == kHitCompact)  // (no lights: the shading reads the material alone)
+        hr[m] = res[m] < 0 ? HitRec{}
+                : a.n_fuse > 0 ? compact_hit(a, u[m], res[m])
+                               : HitRec{V3{}, V3{}, 0.0f, 0.0f, __float_as_uint(a.prim_shade[res[m]].w)};
       else if constexpr (kHit == kHitRecompute) hr[m] = res[m] >= 0 ? recompute_hit(a, u[m], res[m]) : HitRec{};
       else hr[m] = res[m] >= 0 ? load_hit(hit_rec_u(a.hit, u[m])) : HitRec{};
     }
@@ -2347,7 +2353,7 @@ __global__ __launch_bounds__(kBlock, RT_FLAT_WAVES) void flat_render_kernel(Logi
       V3 ro{0.0f, 0.0f, 0.0f};
       if (unit_coords(a, (long long)u, px, py, sample, key)) {
         Rng rng;
-        const Ray cam = sample_ray(a, px, py, sample, key, rng);
+        const Ray cam = sample_ray(a, px, py, sample, key, rng, a.spp_sqrt > 1 || a.cam.aperture > 0.0f || a.op_ft >= 0);
         const float time = a.op_ft >= 0 ? (float)rng.next() : 0.0f;  // camera_kernel's ray-time draw
         ro = cam.o;
         Query q;
