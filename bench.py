@@ -56,7 +56,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 #     4 SIMDs per CU = 2 instructions per CU-cycle (78.6 T lane-ops/s)
 N_CU, MAX_CLOCK_GHZ = 256, 2.4
 SPEC_VALU_WAVE_INSTR_PER_CU_CYCLE = 2.0
-UBENCH_PROFILE = "r06_v5"  # committed counter-measured VALU microbenchmark (profiles/)
+UBENCH_PROFILE = "r06_v6"  # committed counter-measured VALU microbenchmark (profiles/)
 
 
 def valu_peak(path):
@@ -124,7 +124,7 @@ def cpu_baseline_rank(args) -> int | None:
 # one BVH4 node per visit: 80 B in planes-only scenes (fp16 plane codes), 64 B otherwise;
 # one 64-B plane / 128-B transformed record per primitive test
 NODE_BYTES_PLANES, NODE_BYTES_OTHER = 80, 64
-PMC_PROFILE = "r06_v5"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
+PMC_PROFILE = "r06_v6"  # committed rocprofv3 PMC summaries of the headline workload (profiles/)
 
 
 def log(*a):
