@@ -751,8 +751,17 @@ def main():
                        f"{pm.get('frames_per_launch', 1)} frame(s) per profiled launch)")
     if pmc_valu and os.path.exists(pmc_valu):
         pv = json.load(open(pmc_valu))
+    # Few-primitive scenes (at most RT_FLAT_PRIMS bounded primitives, no textures) launch no
+    # traversal: the instrumented frame -- which keeps the traversal launches --
+    # tested them from one leaf item, no node visit; the timed one-pass calls then run
+    # flat_render_kernel and step-pipeline calls a logic step answering its own queries, whose
+    # launches are the "trace" times below
+    textured = args.scene is not None and "texture_file" in open(scene_path).read()
+    flat = cst.node_visits == 0 and cst.prim_tests > 0 and not textured and os.environ.get("RT_FLAT_RENDER", "1") != "0"
     kernel = {
-        "kernel": "trace_refill_kernel", "avg_launch_ms": round(avg_launch_ms, 4),
+        "kernel": ("flat_render_kernel" if flat and one_pass else "logic_kernel (answering its own queries)" if flat
+                   else "trace_refill_kernel"),
+        "avg_launch_ms": round(avg_launch_ms, 4),
         "launches_per_step": round(launches_all / args.steps / world, 3),
         "trace_busy_ms_per_step": round(busy_ms_step, 3),
         # with F > 1 frames in flight the frames' launches overlap: their busy times sum past the
@@ -825,7 +834,11 @@ def main():
             "rng": "counter (splitmix64 per pixel/sample)",
             "frames_in_flight": F,
             "frames_per_call": B,
-            "pipeline": ("one-pass (camera_kernel -> one trace_refill_kernel launch -> shade_reduce_kernel)" if one_pass
+            "pipeline": ("one-pass, few primitives (one flat_render_kernel launch per call: camera ray, queries and "
+                         "shading per thread)" if one_pass and flat
+                         else "one-pass (camera_kernel -> one trace_refill_kernel launch -> shade_reduce_kernel)" if one_pass
+                         else "steps, few primitives (logic -> start over slot state, the logic step answering its own "
+                              "queries: no traversal launches; then reduce)" if flat
                          else "steps (logic -> start -> trace over slot state, then reduce)"),
             **({"emulated_rank": f"{args.emulate_rank}/{args.emulate}"} if args.emulate > 1 and world == 1 else {}),
         },

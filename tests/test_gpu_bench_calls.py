@@ -154,8 +154,8 @@ def test_c3_frame_as_timed(tmp_path, gpu):
     faces and silhouette and the lit floor against the oracle."""
     src, path = _scene_as_bench_writes(tmp_path, "Antialiasing")
     img, line = _bench(tmp_path, "c3", "--scene", src)
-    assert line["config"]["pipeline"].startswith("one-pass") and line["config"]["frames_in_flight"] == 1
-    assert line["config"]["frames_per_call"] == 8
+    assert line["config"]["pipeline"].startswith("one-pass, few primitives") and line["config"]["frames_in_flight"] == 1
+    assert line["config"]["frames_per_call"] == 8 and line["roofline"]["kernel"] == "flat_render_kernel"
     assert np.isfinite(img).all()
     _compare(img, path, 1024, 10, [9 * 16 + 7, 12 * 16 + 6, 7 * 16 + 6, 3 * 16 + 12, 0, 255])
 
@@ -163,11 +163,12 @@ def test_c3_frame_as_timed(tmp_path, gpu):
 def test_c4_frame_as_timed(tmp_path, gpu):
     """C4 as timed: the whole glossy_reflection frame (light radius 1.0, -light_sample 4) on the
     step pipeline with its defaults for scenes with Trace frames -- two slot pipelines on two
-    streams, 8M slots between them (r06), ~40 steps; tiles over the spheres, the cube and their
-    reflections against the oracle."""
+    streams, 8M slots between them, and (five primitives, r06) the logic step answering every
+    query itself, ~13 steps per pipeline and no traversal launch; tiles over the spheres, the cube
+    and their reflections against the oracle."""
     src, path = _scene_as_bench_writes(tmp_path, "glossy_reflection", light_radius=1.0)
     img, line = _bench(tmp_path, "c4", "--scene", src, "--light-radius", "1.0", "--light-samples", "4")
-    assert line["config"]["pipeline"].startswith("steps")
+    assert line["config"]["pipeline"].startswith("steps, few primitives")  # the logic step answers its queries
     assert np.isfinite(img).all()
     tiles_x = 16
     regions = [((t % tiles_x) * T, (t // tiles_x) * T, T, T) for t in [14 * 16 + 7, 10 * 16 + 4, 11 * 16 + 12, 7 * 16 + 9]]
