@@ -756,7 +756,11 @@ def main():
     # tested them from one leaf item, no node visit; the timed one-pass calls then run
     # flat_render_kernel and step-pipeline calls a logic step answering its own queries, whose
     # launches are the "trace" times below
-    textured = args.scene is not None and "texture_file" in open(scene_path).read()
+    def _textured(o) -> bool:  # some material names a texture file (an empty name is none)
+        if isinstance(o, dict):
+            return bool(o.get("texture_file")) or any(_textured(v) for v in o.values())
+        return isinstance(o, list) and any(_textured(v) for v in o)
+    textured = args.scene is not None and _textured(json.load(open(scene_path)))
     flat = cst.node_visits == 0 and cst.prim_tests > 0 and not textured and os.environ.get("RT_FLAT_RENDER", "1") != "0"
     kernel = {
         "kernel": ("flat_render_kernel" if flat and one_pass else "logic_kernel (answering its own queries)" if flat
